@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ray-steps/s of the EC ray-tracing hot path on MI355X.
+
+Workload (BASELINE.json configs[2]): a 100,203-ray EC beam
+(launch_peripheral_rays with N_rings=92, min_azimuthal_points=11) per GPU,
+X-mode, 92.5 GHz, 2,000 fixed RK4 steps of ds = 1e-4 m with Albajar absorption,
+in-kernel psi-shell deposition on a 1,000-point psi grid and a x100-decimated
+trajectory, through the synthetic circular-tokamak equilibrium (56 x 56 grid).
+One "step" of this benchmark = one full pass of the hot path over the beam
+(every ray integrated over its 2,000 RK4 steps) + the RCCL all-reduce of the
+deposited-power profile across ranks.
+
+value = ray-steps actually integrated by all ranks / wall time of the timed
+steps (inputs resident in HBM; ray entry and upload are setup, outside).
+Multi-GPU: one process per GPU (torchrun), each rank traces its own beam
+(rotated toroidally by 2*pi*rank/world; the plasma is axisymmetric), no
+data-path collective; one all_reduce of (n_psi+1) fp64 = make_beam's reduce
+(src/solve.jl:233-240).  scaling = "weak".
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "torj.jl_amd"))
+
+# MI355X fp64 vector peak (spec): 256 CU x 2.4 GHz x 128 flop/clk (64 FMA lanes)
+FP64_VECTOR_PEAK_TFLOPS = 78.6
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n-rings", type=int, default=92)
+    ap.add_argument("--min-az", type=int, default=11)
+    ap.add_argument("--n-steps", type=int, default=2000)
+    ap.add_argument("--ds", type=float, default=1e-4)
+    ap.add_argument("--mode", type=int, default=1)
+    ap.add_argument("--freq", type=float, default=92.5e9)
+    ap.add_argument("--n-psi", type=int, default=1000)
+    ap.add_argument("--traj-stride", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0,
+                    help="target CPU time of the bounded cpu_baseline sample")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import torj_hip as T
+    from torj_hip import flops as F
+    from torj_hip import synthetic as S
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    # ---- setup (outside the timed region) ----
+    eq = S.circular_tokamak()
+    plasma = T.Plasma(*S.plasma_args(eq), device=local)
+    T.abs_Al_init(24)
+    f = args.freq
+    omega = 2 * np.pi * f
+    setup = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(setup["steering_angle_pol"], setup["steering_angle_tor"])
+    x0 = np.array([setup["R0"], 0.0, setup["z0"]])
+    pos, dirs, w = T.launch_peripheral_rays(x0, N0, setup["spot_size"],
+                                            setup["inverse_curvature_radius"], f,
+                                            N_rings=args.n_rings,
+                                            min_azimuthal_points=args.min_az)
+    phi = 2 * np.pi * rank / max(world, 1)  # weak scaling: each rank its own (rotated) beam
+    rot = np.array([[np.cos(phi), -np.sin(phi), 0], [np.sin(phi), np.cos(phi), 0], [0, 0, 1]])
+    pos, dirs = pos @ rot.T, dirs @ rot.T
+    xp, Np, s0, st = T.ray_entry(plasma, pos, dirs, omega, args.mode)
+    if not (st == 0).all():
+        raise RuntimeError(f"ray entry failed for {(st != 0).sum()} rays")
+    n = len(w)
+    grid = np.linspace(0.0, 1.0, args.n_psi)
+
+    def dev_t(a, dtype=torch.float64):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dtype)
+
+    d_x0, d_N0, d_w, d_grid = dev_t(xp.T), dev_t(Np.T), dev_t(w), dev_t(grid)
+    d_state = torch.empty((7, n), dtype=torch.float64, device=dev)
+    d_status = torch.empty(n, dtype=torch.int32, device=dev)
+    d_steps = torch.empty(n, dtype=torch.int32, device=dev)
+    d_dP = torch.zeros(args.n_psi + 1, dtype=torch.float64, device=dev)
+    d_Pdep = torch.empty(n, dtype=torch.float64, device=dev)
+    n_save = args.n_steps // args.traj_stride if args.traj_stride > 0 else 0
+    d_traj = torch.empty((max(n_save, 1), 4, n), dtype=torch.float64, device=dev)
+    d_cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    cfg = T._lib.TraceCfg(omega, args.mode, args.ds, args.n_steps, max(1, args.n_steps // 100),
+                          1.0, 1e-6, 1, args.traj_stride)
+    L = T.lib()
+    stream = torch.cuda.current_stream(dev)
+
+    def launch(counters=None):
+        d_dP.zero_()
+        T._lib.check(L.torj_trace_device(
+            plasma.handle, cfg, n, d_x0.data_ptr(), d_N0.data_ptr(), d_w.data_ptr(), args.n_psi,
+            d_grid.data_ptr(), d_state.data_ptr(), d_status.data_ptr(), d_steps.data_ptr(),
+            d_dP.data_ptr(), d_Pdep.data_ptr(), d_traj.data_ptr() if n_save else None,
+            counters, stream.cuda_stream))
+
+    def one_step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        launch()
+        if ev is not None:
+            ev[1].record(stream)
+        if world > 1:
+            dist.all_reduce(d_dP)  # RCCL over xGMI: (n_psi+1) fp64, make_beam's reduce
+
+    # counted launch (work counters for the algorithmic FLOP figure), also warms up
+    d_cnt.zero_()
+    launch(d_cnt.data_ptr())
+    torch.cuda.synchronize(dev)
+    cnt = d_cnt.cpu().numpy().astype(np.int64)
+    ray_steps_local = int(cnt[0])
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        one_step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    tot_steps = torch.tensor([ray_steps_local], dtype=torch.float64, device=dev)
+    el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tot_steps)
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    ray_steps_all = float(tot_steps.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    value = ray_steps_all / (ms_per_step / 1e3)
+
+    if rank == 0:
+        status = d_status.cpu().numpy()
+        flop = F.algorithmic_flops(cnt, n_gl=24)
+        kern_s = float(km.item()) / 1e3
+        achieved = flop / kern_s / 1e12
+        out = {
+            "metric": "ray-steps/sec, 1e5-ray EC fan on 1 MI355X (+ 2/4/8-GPU scaling)",
+            "value": value,
+            "unit": "ray-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic circular-tokamak equilibrium (analytic, sampled on 56x56) + "
+                    "launch_peripheral_rays fan",
+            "config": {
+                "workload": f"C3: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
+                            f"min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, {args.n_steps} RK4 "
+                            f"steps ds={args.ds:g} m, Albajar alpha (GL-24), psi-shell deposition "
+                            f"n_psi={args.n_psi}, traj stride {args.traj_stride}",
+                "rays_per_gpu": n,
+                "rk4_steps": args.n_steps,
+                "parallelism": f"ray-shard x{world} + RCCL all_reduce of dP/dV",
+                "ray_status_counts": {T.STATUS_NAMES[i]: int(c)
+                                      for i, c in enumerate(np.bincount(status, minlength=6)) if c},
+            },
+            "roofline": {
+                "bound": "fp64-valu",
+                "achieved": achieved,
+                "peak": FP64_VECTOR_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
+                "traffic": None,
+                "kernel": "k_trace<ABS,DEPO,TRAJ>",
+                "kernel_ms": kern_s * 1e3,
+                "algorithmic_flop_per_launch": flop,
+                "flop_per_ray_step": flop / max(cnt[0], 1),
+            },
+            "work_counters": {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
+                              "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(eq, xp, Np, w, omega, args, grid):
+    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same rays."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from torj_hip import synthetic as S
+
+    OP = O.OraclePlasma(*S.plasma_args(eq))
+    O.abs_al_init(24)
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or 1)
+    idx = np.linspace(0, len(w) - 1, num=threads, dtype=int)  # calibration sample
+    t0 = time.perf_counter()
+    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, psi_grid=grid,
+                 weights=w[idx], n_threads=threads)
+    t_cal = time.perf_counter() - t0
+    n_rays = int(max(threads, min(len(w), threads * max(1, round(args.cpu_seconds / max(t_cal, 1e-3))))))
+    idx = np.linspace(0, len(w) - 1, num=n_rays, dtype=int)
+    t0 = time.perf_counter()
+    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, psi_grid=grid,
+                 weights=w[idx], n_threads=threads)
+    dt = time.perf_counter() - t0
+    steps = int(r["steps"].sum())
+    return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
+            "sample": f"{n_rays} rays (evenly spaced over the same fan) x {args.n_steps} RK4 steps, "
+                      f"oracle/torj_oracle.c OpenMP, {steps} ray-steps in {dt:.1f} s"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,178 @@
+/*
+ * torj_hip.h -- C ABI of libtorj_hip.so, the MI355X-native replacement for the
+ * ray-tracing hot path of TorJ.jl (make_ray / make_beam, src/solve.jl).
+ *
+ * The reference has no FFI: everything is Julia.  Each entry point below names
+ * the Julia function whose behaviour it replaces (file:line in the TorJ.jl
+ * repository); INTEGRATION.md shows the `ccall` bindings a TorJ maintainer
+ * would add (torj.jl_amd/julia/TorJHIP.jl) and the Python ctypes mirror used by
+ * this repository's tests (torj.jl_amd/torj_hip).
+ *
+ * Conventions
+ *  - Plain C types only.  Return value: 0 = success, <0 = error; the message of
+ *    the last error on the calling thread is returned by torj_last_error().
+ *    No exception or longjmp ever crosses this boundary.
+ *  - Per-ray 3-vectors are COMPONENT-MAJOR ("SoA"): v[c*n + i] is component c of
+ *    ray i.  This is exactly the memory of a Julia `n x 3` Matrix{Float64}
+ *    (column-major), e.g. the ray_positions returned by launch_peripheral_rays
+ *    (src/launch.jl:84-86), so Julia passes them without copying.
+ *  - 2-D maps are (nR x nZ) column-major (R fastest), i.e. Julia matrices.
+ *  - Functions without the _device suffix take HOST pointers owned by the
+ *    caller and valid only for the call (Julia: GC.@preserve); they copy to the
+ *    GPU, run, copy back and synchronise.  *_device functions take device
+ *    pointers and a hipStream_t (as void*), enqueue and return immediately.
+ *  - All arithmetic is fp64.
+ *  - Every compute entry point runs on the GPU (HIP, gfx950).  There is no
+ *    CPU fallback: without a usable GPU they return an error.
+ */
+#ifndef TORJ_HIP_H
+#define TORJ_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TORJ_ABI_VERSION 1
+
+/* per-ray status codes (replace the reference's @assert / unhandled returns) */
+enum torj_status {
+    TORJ_RAY_OK = 0,          /* ran all steps */
+    TORJ_RAY_LEFT_PLASMA = 1, /* psi > psi_exit at a chunk boundary (src/solve.jl:174) */
+    TORJ_RAY_ABSORBED = 2,    /* P < P_min at a chunk boundary (src/solve.jl:176) */
+    TORJ_RAY_NAN = 3,         /* non-finite state (e.g. upper-hybrid resonance) */
+    TORJ_RAY_REFLECTED = 4,   /* N_s^2 <= 0 at the plasma edge (src/solve.jl:57-59) */
+    TORJ_RAY_ENTRY_FAIL = 5   /* first_point / refraction assertions (src/solve.jl:32,138,141) */
+};
+
+typedef struct torj_plasma_s *torj_plasma_t;
+
+/* ---- library / device ---------------------------------------------------- */
+int torj_abi_version(void);
+const char *torj_last_error(void);
+int torj_device_count(int *n);
+
+/* abs_Al_init(N_absz) (src/absorption.jl:1-7): Gauss-Legendre order of the
+ * Albajar resonance-ellipse integral (process-global, like the reference's
+ * module globals _int_absz/_int_weights, src/constants.jl:7-8).  1 <= n <= 64.
+ * Absorption calls fail with the reference's ErrorException message
+ * (src/absorption.jl:173-175) until this has been called. */
+int torj_abs_al_init(int n);
+
+/* ---- Plasma (src/plasma.jl:2-58) ----------------------------------------- */
+/* Plasma(R_coords, Z_coords, psi_norm_data, psi_prof, ne_prof, Te_prof, Br_data,
+ *        Bz_data, Bϕ_data, eqt1d_psi_norm, eqt1d_volume)   (src/plasma.jl:30-58)
+ * Builds the Interpolations.jl-equivalent cubic B-spline coefficients (Line()
+ * boundary/extrapolation) on the host and uploads them to `device`. */
+int torj_plasma_create(int nR, int nZ, const double *R_coords, const double *Z_coords,
+                       const double *psi_norm_data, int n_prof, const double *psi_prof,
+                       const double *ne_prof, const double *Te_prof, const double *Br_data,
+                       const double *Bz_data, const double *Bphi_data, int n_eq,
+                       const double *eqt1d_psi_norm, const double *eqt1d_volume, int device,
+                       torj_plasma_t *out);
+/* Same, from B-spline coefficient arrays already built by Interpolations.jl
+ * (parent(spl.itp.itp.coefs): (nR+2) x (nZ+2) column-major each; field order
+ * psi, ln ne, ln Te, Br, Bz, Bphi) and the 1-D volume spline coefficients
+ * (n_vol+2 over the uniform psi range [vol_psi1, vol_psin]). */
+int torj_plasma_create_from_coefs(int nR, int nZ, double R1, double Rn, double Z1, double Zn,
+                                  const double *coef_psi, const double *coef_lnne,
+                                  const double *coef_lnTe, const double *coef_Br,
+                                  const double *coef_Bz, const double *coef_Bphi, int n_vol,
+                                  double vol_psi1, double vol_psin, const double *vol_coefs,
+                                  double psi_prof_max, int device, torj_plasma_t *out);
+int torj_plasma_destroy(torj_plasma_t p);
+/* field: 0 psi, 1 ln ne, 2 ln Te, 3 Br, 4 Bz, 5 Bphi.  out: (nR+2)*(nZ+2), column-major */
+int torj_plasma_get_coefs(torj_plasma_t p, int field, double *out);
+double torj_plasma_psi_prof_max(torj_plasma_t p);
+/* plasma.volume_psi_spline at n points (host) */
+int torj_plasma_volume(torj_plasma_t p, int n, const double *psi, double *vol);
+
+/* ---- point evaluations (GPU; mirror the reference's unit-tested functions) -- */
+/* Per point i (x, N component-major 3 x n), out is 13 x n component-major:
+ *   0-2  B_spline(plasma, x)            (src/plasma.jl:73-81)
+ *   3    n_e(plasma, x)                 (src/plasma.jl:83-85)
+ *   4    T_e(plasma, x)                 (src/plasma.jl:87-89)
+ *   5    evaluate(psi_norm_spline, x)   (src/plasma.jl:61-65)
+ *   6-8  X, Y, N_par of eval_plasma     (src/dispersion.jl:7-15)
+ *   9-11 b of eval_plasma
+ *   12   |B|                                                             */
+int torj_eval_plasma(torj_plasma_t p, int n, const double *x, const double *N, double omega,
+                     double *out);
+/* dispersion_relation (src/dispersion.jl:34-39), the normalised Hamiltonian
+ * RHS of gradΛ! (src/solve.jl:85-93; du = dx/ds, dN/ds, 6 x n) and α_approx
+ * (src/absorption.jl:228-235; pass alpha = NULL to skip). */
+int torj_dispersion(torj_plasma_t p, int n, const double *x, const double *N, double omega,
+                    int mode, double *D, double *du, double *alpha);
+/* abs_Albajar_fast(omega, X, Y, N_abs, N_par, Te, mode) (src/absorption.jl:191-226),
+ * batched over n tuples (arrays of length n). */
+int torj_abs_albajar_fast(int n, const double *omega, const double *X, const double *Y,
+                          const double *N_abs, const double *N_par, const double *Te, int mode,
+                          double *alpha);
+/* refractive_index_sq(X, Y, N_par, mode) (src/dispersion.jl:29-32), batched */
+int torj_refractive_index_sq(int n, const double *X, const double *Y, const double *N_par,
+                             int mode, double *out);
+
+/* ---- launch (host) ------------------------------------------------------- */
+/* IMAS.pol_tor_angles_2_vector(pol, tor) as called at src/solve.jl:211 */
+void torj_pol_tor_angles_2_vector(double pol, double tor, double N[3]);
+/* launch_peripheral_rays (src/launch.jl:24-132).  Call with pos == NULL to get
+ * the ray count in *n_rays; then with arrays of that size (pos, dir
+ * component-major 3 x n).  Returns -1 (ArgumentError) for N_rings < 2. */
+int torj_launch_peripheral_rays(const double x0[3], const double N0[3], double w,
+                                double inverse_curvature_radius, double f, int N_rings,
+                                int min_azimuthal_points, int normalize_weight_sum, int *n_rays,
+                                double *pos, double *dir, double *weights);
+
+/* ---- ray entry: first_point + vacuum_plasma_refraction (src/solve.jl:7-74) --
+ * x0, N0: vacuum launch points/directions (3 x n); outputs the in-plasma start
+ * point, refracted N, vacuum path length s0 and a status per ray. */
+int torj_ray_entry(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
+                   int mode, double *x_plasma, double *N_plasma, double *s0, int *status);
+
+/* ---- the hot path: ray stepping (src/solve.jl:144-177) ------------------- */
+typedef struct {
+    double omega;     /* 2 pi f */
+    int mode;         /* +1 X-mode, -1 O-mode (src/solve.jl:110) */
+    double ds;        /* fixed RK4 step [m]; the reference caps dtmax at 1e-4 (src/solve.jl:157) */
+    int n_steps;      /* steps per ray (s_max / ds) */
+    int chunk_steps;  /* termination checks every chunk_steps (reference: 100 chunks, src/solve.jl:145) */
+    double psi_exit;  /* 1.0 in the reference (src/solve.jl:174) */
+    double P_min;     /* 1e-6 in the reference (src/solve.jl:176) */
+    int absorption;   /* 1: integrate optical depth with abs_Albajar_fast */
+    int traj_stride;  /* 0: no trajectory; else save (x,y,z,tau) every traj_stride steps */
+} torj_trace_cfg;
+
+/* Host-pointer form.  x0, N0: in-plasma start states (3 x n); weights (n, may
+ * be NULL = all 1); psi_grid (n_psi, may be n_psi = 0: no deposition).
+ * Outputs: state 7 x n (x, y, z, Nx, Ny, Nz, tau with P = exp(-tau)),
+ * status n, steps n; dP_shell n_psi + 1: [j] = sum_rays w * (power deposited
+ * in psi shell [psi_grid[j], psi_grid[j+1]]) for j < n_psi-1, [n_psi-1] = 0,
+ * [n_psi] = sum_rays w * P_dep(ray); P_dep n (per ray, unweighted).  traj:
+ * (n_steps/traj_stride) x 4 x n, NaN after a ray stops.  Any output may be
+ * NULL.  Divide dP_shell[j] by the shell volume to get make_beam's dP_dV
+ * (src/plasma.jl:141, src/solve.jl:237-240). */
+int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+               const double *N0, const double *weights, int n_psi, const double *psi_grid,
+               double *state, int *status, int *steps, double *dP_shell, double *P_dep,
+               double *traj);
+
+/* Device-pointer form (inputs resident in HBM; what bench.py times).
+ * dP_shell (n_psi+1) is ACCUMULATED into (zero it first).  counters (may be
+ * NULL): 4 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
+ * reaching the harmonic sum, harmonic integrals -- the basis of the algorithmic
+ * FLOP count.  stream: hipStream_t or NULL. */
+int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                      const double *N0, const double *weights, int n_psi,
+                      const double *psi_grid, double *state, int *status, int *steps,
+                      double *dP_shell, double *P_dep, double *traj, uint64_t *counters,
+                      void *stream);
+
+/* shell volumes dV[j] = V(psi_grid[j+1]) - V(psi_grid[j]), j < n_psi-1 (host;
+ * src/plasma.jl:117-122) */
+int torj_shell_volumes(torj_plasma_t p, int n_psi, const double *psi_grid, double *dV);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TORJ_HIP_H */

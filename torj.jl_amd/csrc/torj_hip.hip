@@ -1,0 +1,1294 @@
+// torj_hip.hip -- libtorj_hip.so: HIP (gfx950) kernels for TorJ.jl's ray-tracing
+// hot path plus the C ABI declared in include/torj_hip.h.
+//
+// Layout of work:
+//   k_trace<ABS,DEPO,TRAJ>  one lane per ray; the whole make_ray integration loop
+//                           (src/solve.jl:154-177) runs in registers: fixed-step
+//                           RK4 of gradΛ!/sys! (src/solve.jl:85-114), optical
+//                           depth from abs_Albajar_fast (src/absorption.jl:191-226),
+//                           chunk-granular termination, psi-shell deposition
+//                           accumulated per lane and flushed with fp64 atomics.
+//   k_eval_plasma / k_dispersion / k_albajar / k_refr
+//                           batched point evaluations mirroring the reference's
+//                           unit-tested functions (test_trajectory.jl, test_absorption.jl).
+// Host side (this file): Plasma construction (Interpolations.jl-equivalent
+// prefilter), the launch fan and the ray entry -- setup work the reference also
+// does per beam/ray on the CPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/torj_hip.h"
+#include "torj_math.hpp"
+
+using namespace torj;
+
+// ===========================================================================
+// error handling
+// ===========================================================================
+static thread_local std::string g_err;
+
+static int fail(const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return -1;
+}
+
+#define HIPCK(expr)                                                                       \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail("%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// ===========================================================================
+// Gauss-Legendre table in constant memory (abs_Al_init, src/absorption.jl:1-7)
+// ===========================================================================
+__constant__ GLTable c_gl;
+
+static std::mutex g_gl_mu;
+static GLTable g_gl_host;
+static int g_gl_version = 0;         // 0: abs_Al_init never called
+static int g_gl_uploaded[64] = {0};  // per device
+
+static void gauss_legendre(int n, double *x, double *w) {
+    const int m = (n + 1) / 2;
+    for (int i = 0; i < m; i++) {
+        double z = std::cos(kPi * (i + 0.75) / (n + 0.5)), pp = 1.0;
+        for (int it = 0; it < 100; it++) {
+            double p0 = 1.0, p1 = z;  // P_0, P_1
+            for (int j = 2; j <= n; j++) {
+                const double p2 = ((2.0 * j - 1.0) * z * p1 - (j - 1.0) * p0) / j;
+                p0 = p1;
+                p1 = p2;
+            }
+            if (n == 1) p0 = 1.0, p1 = z;
+            pp = n * (z * p1 - p0) / (z * z - 1.0);
+            const double dz = p1 / pp;
+            z -= dz;
+            if (std::fabs(dz) < 1e-16) break;
+        }
+        x[i] = -z;
+        x[n - 1 - i] = z;
+        w[i] = w[n - 1 - i] = 2.0 / ((1.0 - z * z) * pp * pp);
+    }
+}
+
+static int ensure_gl_on_device(int dev) {
+    std::lock_guard<std::mutex> lk(g_gl_mu);
+    if (g_gl_version == 0)
+        return fail(
+            "The weights and abscissae for the absorption were never initialized. Call "
+            "`abs_Al_init` before using the absorption.");
+    if (dev < 0 || dev >= 64) return fail("device index %d out of range", dev);
+    if (g_gl_uploaded[dev] != g_gl_version) {
+        HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(c_gl), &g_gl_host, sizeof(GLTable)));
+        g_gl_uploaded[dev] = g_gl_version;
+    }
+    return 0;
+}
+
+// ===========================================================================
+// kernels
+// ===========================================================================
+struct TraceArgs {
+    const double *coef;
+    Grid g;
+    Consts k;
+    double omega;
+    int mode;
+    double ds;
+    int n_steps;
+    int chunk_steps;
+    double psi_exit;
+    double P_min;
+    int n;
+    const double *x0;  // 3 x n
+    const double *N0;  // 3 x n
+    const double *w;   // n or null
+    double *state;     // 7 x n
+    int *status;
+    int *steps;
+    int n_psi;
+    const double *grid;
+    int grid_uniform;
+    double g0, ginv;
+    double *dP;  // n_psi + 1
+    double *Pdep;
+    int traj_stride;
+    int n_save;
+    double *traj;  // n_save x 4 x n
+    unsigned long long *counters;
+};
+
+// psi shell j with grid[j] <= v < grid[j+1], clamped to [0, n-2]; identical
+// result to a binary search on the grid array.
+__device__ __forceinline__ int shell_of(const TraceArgs &a, double v) {
+    const int nm2 = a.n_psi - 2;
+    int j;
+    if (a.grid_uniform) {
+        j = (int)floor((v - a.g0) * a.ginv);
+        j = j < 0 ? 0 : (j > nm2 ? nm2 : j);
+        while (j > 0 && a.grid[j] > v) j--;
+        while (j < nm2 && a.grid[j + 1] <= v) j++;
+    } else {
+        int lo = 0, hi = a.n_psi - 1;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.grid[mid] <= v)
+                lo = mid;
+            else
+                hi = mid;
+        }
+        j = lo;
+    }
+    return j;
+}
+
+struct DepoAcc {
+    int cur;
+    double acc;
+};
+
+__device__ __forceinline__ void depo_add(const TraceArgs &a, DepoAcc &d, int j, double v) {
+    if (j == d.cur) {
+        d.acc += v;
+    } else {
+        if (d.cur >= 0) atomicAdd(a.dP + d.cur, d.acc);
+        d.cur = j;
+        d.acc = v;
+    }
+}
+
+// power dP deposited over a step whose psi runs linearly pa -> pb
+__device__ __forceinline__ double deposit(const TraceArgs &a, DepoAcc &d, double pa, double pb,
+                                          double dP, double w) {
+    if (!(dP != 0.0)) return 0.0;
+    const double lo = pa < pb ? pa : pb, hi = pa < pb ? pb : pa;
+    const double g0 = a.grid[0], gl = a.grid[a.n_psi - 1];
+    if (hi == lo) {
+        if (lo < g0 || lo > gl) return 0.0;
+        depo_add(a, d, shell_of(a, lo), w * dP);
+        return dP;
+    }
+    if (hi <= g0 || lo >= gl) return 0.0;
+    const double span = hi - lo;
+    double inside = 0.0;
+    for (int j = shell_of(a, lo < g0 ? g0 : lo); j < a.n_psi - 1 && a.grid[j] < hi; j++) {
+        const double gj = a.grid[j], gj1 = a.grid[j + 1];
+        const double x0 = lo > gj ? lo : gj, x1 = hi < gj1 ? hi : gj1;
+        if (x1 <= x0) continue;
+        const double part = dP * ((x1 - x0) / span);
+        depo_add(a, d, j, w * part);
+        inside += part;
+    }
+    return inside;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <bool ABS, bool DEPO, bool TRAJ>
+__global__ void __launch_bounds__(256, 2) k_trace(TraceArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = i < a.n;
+    const GLTable &gl = c_gl;
+    AlbajarWork work = {0u, 0u};
+    int steps = 0;
+    if (live) {
+        double x[3], N[3];
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = a.x0[c * a.n + i];
+            N[c] = a.N0[c * a.n + i];
+        }
+        const double w = (DEPO && a.w) ? a.w[i] : 1.0;
+        double tau = 0.0, P = 1.0;
+        int status = ST_OK;
+        double psi_a = 0.0;
+        DepoAcc dacc = {-1, 0.0};
+        double Pdep = 0.0;
+        if constexpr (DEPO) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+        const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
+        for (int s = 0; s < a.n_steps; s++) {
+            // classic RK4 with a single RHS call site (keeps one copy of the
+            // spline + Albajar code live -> lower VGPR pressure)
+            double acc[6] = {0, 0, 0, 0, 0, 0}, acc_a = 0.0, xt[3], Nt[3], k[6], al;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                xt[c] = x[c];
+                Nt[c] = N[c];
+            }
+#pragma unroll 1
+            for (int st = 0; st < 4; st++) {
+                ray_rhs<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, xt, Nt, k, al, &work);
+                const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
+                const double h = (st < 2) ? hds : ds;
+#pragma unroll
+                for (int c = 0; c < 6; c++) acc[c] = fma(wgt, k[c], acc[c]);
+                acc_a = fma(wgt, al, acc_a);
+#pragma unroll
+                for (int c = 0; c < 3; c++) {
+                    xt[c] = fma(h, k[c], x[c]);
+                    Nt[c] = fma(h, k[3 + c], N[c]);
+                }
+            }
+            double xn[3], Nn[3];
+            bool bad = false;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                xn[c] = x[c] + ds6 * acc[c];
+                Nn[c] = N[c] + ds6 * acc[3 + c];
+                bad |= !isfinite(xn[c]) || !isfinite(Nn[c]);
+            }
+            const double taun = tau + ds6 * acc_a;
+            bad |= !isfinite(taun);
+            if (bad) {
+                status = ST_NAN;
+                break;
+            }
+            const double Pn = exp(-taun);
+            const double dP = P - Pn;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                x[c] = xn[c];
+                N[c] = Nn[c];
+            }
+            tau = taun;
+            P = Pn;
+            steps = s + 1;
+            const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
+            double psi_b = 0.0;
+            if (DEPO || check) psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+            if constexpr (DEPO) {
+                Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
+                psi_a = psi_b;
+            }
+            if constexpr (TRAJ) {
+                if ((steps % a.traj_stride) == 0) {
+                    const size_t si = (size_t)(steps / a.traj_stride - 1);
+                    double *T = a.traj + si * 4 * (size_t)a.n + i;
+                    T[0] = x[0];
+                    T[(size_t)a.n] = x[1];
+                    T[2 * (size_t)a.n] = x[2];
+                    T[3 * (size_t)a.n] = tau;
+                }
+            }
+            if (check) {
+                if (psi_b > a.psi_exit) {  // src/solve.jl:174
+                    status = ST_LEFT_PLASMA;
+                    break;
+                }
+                if (P < a.P_min) {  // src/solve.jl:176
+                    status = ST_ABSORBED;
+                    break;
+                }
+            }
+        }
+        if constexpr (DEPO) {
+            if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
+            if (a.Pdep) a.Pdep[i] = Pdep;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            a.state[c * a.n + i] = x[c];
+            a.state[(3 + c) * a.n + i] = N[c];
+        }
+        a.state[6 * a.n + i] = tau;
+        a.status[i] = status;
+        a.steps[i] = steps;
+        if constexpr (DEPO) {
+            // beam deposited power sum_rays w * P_dep(ray) in slot n_psi
+            double v = w * Pdep;
+            atomicAdd(a.dP + a.n_psi, v);
+        }
+    }
+    if (a.counters) {
+        const unsigned long long s0 = wave_sum((unsigned long long)steps);
+        const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
+        const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(a.counters + 0, s0);
+            atomicAdd(a.counters + 1, 4ull * s0);
+            atomicAdd(a.counters + 2, s2);
+            atomicAdd(a.counters + 3, s3);
+        }
+    }
+}
+
+struct EvalArgs {
+    const double *coef;
+    Grid g;
+    Consts k;
+    double omega;
+    int mode;
+    int n;
+    const double *x, *N;
+    double *out;
+    double *D, *du, *alpha;
+};
+
+__global__ void __launch_bounds__(256, 1) k_eval_plasma(EvalArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    double x[3], N[3];
+    for (int c = 0; c < 3; c++) {
+        x[c] = a.x[c * a.n + i];
+        N[c] = a.N[c * a.n + i];
+    }
+    PlasmaPoint p;
+    plasma_point<true>(a.coef, a.g, a.k, x, p);
+    const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
+    double *o = a.out;
+    const size_t n = a.n;
+    o[0 * n + i] = p.B[0];
+    o[1 * n + i] = p.B[1];
+    o[2 * n + i] = p.B[2];
+    o[3 * n + i] = p.ne;
+    o[4 * n + i] = exp(p.lnTe);
+    o[5 * n + i] = eval_one(a.coef, a.g, R, x[2], F_PSI);
+    o[6 * n + i] = p.X;
+    o[7 * n + i] = p.Y;
+    o[8 * n + i] = N[0] * p.b[0] + N[1] * p.b[1] + N[2] * p.b[2];
+    o[9 * n + i] = p.b[0];
+    o[10 * n + i] = p.b[1];
+    o[11 * n + i] = p.b[2];
+    o[12 * n + i] = p.Babs;
+}
+
+template <bool ABS>
+__global__ void __launch_bounds__(256, 1) k_dispersion(EvalArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    double x[3], N[3], du[6], alpha;
+    for (int c = 0; c < 3; c++) {
+        x[c] = a.x[c * a.n + i];
+        N[c] = a.N[c * a.n + i];
+    }
+    PlasmaPoint p;
+    plasma_point<ABS>(a.coef, a.g, a.k, x, p);
+    double Npar;
+    const double D = dispersion_grad(p, N, a.mode, du, &Npar);
+    if (a.D) a.D[i] = D;
+    if (a.du)
+        for (int c = 0; c < 6; c++) a.du[c * a.n + i] = du[c];
+    if constexpr (ABS) {
+        const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+        alpha = abs_albajar_fast(c_gl, a.omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), a.mode, nullptr);
+        a.alpha[i] = alpha;
+    }
+}
+
+struct AlbArgs {
+    int n, mode;
+    const double *omega, *X, *Y, *Nabs, *Npar, *Te;
+    double *out;
+};
+
+__global__ void __launch_bounds__(256, 1) k_albajar(AlbArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    a.out[i] = abs_albajar_fast(c_gl, a.omega[i], a.X[i], a.Y[i], a.Nabs[i], a.Npar[i], a.Te[i],
+                                a.mode, nullptr);
+}
+
+__global__ void k_refr(AlbArgs a) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= a.n) return;
+    a.out[i] = refractive_index_sq(a.X[i], a.Y[i], a.Npar[i], a.mode);
+}
+
+// ===========================================================================
+// Plasma construction (host), src/plasma.jl:16-58
+// ===========================================================================
+// Cubic{Line{OnGrid}} prefilter of Interpolations.jl.  The boundary rows
+// c0 - 2c1 + c2 = 0 combined with the first interpolation row give c1 = y1
+// (same at the far end), leaving a [1 4 1]/6 tridiagonal system for the
+// interior coefficients (solved with the Thomas algorithm).
+static void bspl1d_prefilter(int n, const double *y, size_t ystride, double *c, size_t cstride) {
+    // c has n+2 entries
+    auto C = [&](int k) -> double & { return c[(size_t)k * cstride]; };
+    auto Y = [&](int k) { return y[(size_t)k * ystride]; };
+    C(1) = Y(0);
+    C(n) = Y(n - 1);
+    const int m = n - 2;  // interior unknowns c_2..c_{n-1}
+    if (m > 0) {
+        std::vector<double> cp(m), dp(m);
+        for (int k = 0; k < m; k++) {
+            double r = 6.0 * Y(k + 1);
+            if (k == 0) r -= C(1);
+            if (k == m - 1) r -= C(n);
+            const double den = 4.0 - (k > 0 ? cp[k - 1] : 0.0);
+            cp[k] = 1.0 / den;
+            dp[k] = (r - (k > 0 ? dp[k - 1] : 0.0)) / den;
+        }
+        C(m + 1) = dp[m - 1];
+        for (int k = m - 2; k >= 0; k--) C(k + 2) = dp[k] - cp[k] * C(k + 3);
+    }
+    C(0) = 2.0 * C(1) - C(2);
+    C(n + 1) = 2.0 * C(n) - C(n - 1);
+}
+
+// y: nR x nZ (R fastest) -> c: (nR+2) x (nZ+2) (R fastest)
+static void bspl2d_prefilter(int nR, int nZ, const double *y, double *c) {
+    const int mR = nR + 2, mZ = nZ + 2;
+    std::fill(c, c + (size_t)mR * mZ, 0.0);
+    for (int j = 0; j < nZ; j++)
+        bspl1d_prefilter(nR, y + (size_t)j * nR, 1, c + (size_t)(j + 1) * mR, 1);
+    std::vector<double> row(nZ);
+    for (int i = 0; i < mR; i++) {
+        for (int j = 0; j < nZ; j++) row[j] = c[(size_t)(j + 1) * mR + i];
+        bspl1d_prefilter(nZ, row.data(), 1, c + i, (size_t)mR);
+    }
+}
+
+static double bspl1d_eval(const std::vector<double> &c, int n, double x1, double xn, double x) {
+    const double h = (xn - x1) / (n - 1);
+    const double xc = clampd(x, x1, xn);
+    const double u = (xc - x1) / h;
+    int i = (int)std::floor(u);
+    i = std::max(0, std::min(n - 2, i));
+    double w[4], dw[4];
+    bweights(u - i, w, dw);
+    double v = 0, g = 0;
+    for (int a = 0; a < 4; a++) {
+        v += w[a] * c[i + a];
+        g += dw[a] * c[i + a];
+    }
+    return v + (x - xc) * (g / h);
+}
+
+// natural cubic spline through (x, y) evaluated at xq (IMAS.interp1d :cubic;
+// parity unpinned -- exact at the nodes, so any interpolant agrees when the
+// profile grid is already uniform)
+static void natcubic(int n, const double *x, const double *y, int nq, const double *xq,
+                     double *yq) {
+    std::vector<double> M(n, 0.0);
+    if (n >= 3) {
+        const int m = n - 2;
+        std::vector<double> a(m), b(m), c(m), r(m);
+        for (int i = 1; i <= m; i++) {
+            const double h0 = x[i] - x[i - 1], h1 = x[i + 1] - x[i];
+            a[i - 1] = h0;
+            b[i - 1] = 2.0 * (h0 + h1);
+            c[i - 1] = h1;
+            r[i - 1] = 6.0 * ((y[i + 1] - y[i]) / h1 - (y[i] - y[i - 1]) / h0);
+        }
+        for (int i = 1; i < m; i++) {
+            const double f = a[i] / b[i - 1];
+            b[i] -= f * c[i - 1];
+            r[i] -= f * r[i - 1];
+        }
+        M[m] = r[m - 1] / b[m - 1];
+        for (int i = m - 1; i >= 1; i--) M[i] = (r[i - 1] - c[i - 1] * M[i + 1]) / b[i - 1];
+    }
+    for (int q = 0; q < nq; q++) {
+        const double t = xq[q];
+        const int i = std::max(0, std::min(n - 2, (int)(std::upper_bound(x, x + n, t) - x) - 1));
+        if (t == x[i]) {
+            yq[q] = y[i];
+            continue;
+        }
+        if (t == x[i + 1]) {
+            yq[q] = y[i + 1];
+            continue;
+        }
+        const double h = x[i + 1] - x[i], A = x[i + 1] - t, B = t - x[i];
+        yq[q] = M[i] * A * A * A / (6.0 * h) + M[i + 1] * B * B * B / (6.0 * h) +
+                (y[i + 1] / h - M[i + 1] * h / 6.0) * B + (y[i] / h - M[i] * h / 6.0) * A;
+    }
+}
+
+static std::vector<double> uniform_range(double a, double b, int n) {
+    std::vector<double> r(n);
+    for (int i = 0; i < n; i++) r[i] = a + (b - a) * i / (n - 1.0);
+    r[n - 1] = b;
+    return r;
+}
+
+struct torj_plasma_s {
+    int device = 0;
+    Grid g{};
+    std::vector<double> coef;  // interleaved host copy
+    double *d_coef = nullptr;
+    int n_vol = 0;
+    double v1 = 0, vn = 0;
+    std::vector<double> vol_coef;
+    double psi_prof_max = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+};
+
+static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
+
+static int plasma_finish(torj_plasma_s *p, int nR, int nZ, double R1, double Rn, double Z1,
+                         double Zn, const double *const fields[6], int device,
+                         torj_plasma_t *out) {
+    p->device = device;
+    Grid &g = p->g;
+    g.nR = nR;
+    g.nZ = nZ;
+    g.R1 = R1;
+    g.Rn = Rn;
+    g.Z1 = Z1;
+    g.Zn = Zn;
+    g.hR = (Rn - R1) / (nR - 1);
+    g.hZ = (Zn - Z1) / (nZ - 1);
+    g.invhR = 1.0 / g.hR;
+    g.invhZ = 1.0 / g.hZ;
+    const size_t nodes = (size_t)(nR + 2) * (nZ + 2);
+    p->coef.assign(nodes * kNF, 0.0);
+    for (int f = 0; f < 6; f++)
+        for (size_t k = 0; k < nodes; k++) p->coef[k * kNF + kFieldSlot[f]] = fields[f][k];
+    *out = p;
+    return 0;
+}
+
+// Device-side state is created on first GPU use, so the host-side parts of
+// the ABI (Plasma construction, ray entry, launch fan) work without a GPU.
+static int ensure_device(torj_plasma_s *p) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    int ndev = 0;
+    HIPCK(hipGetDeviceCount(&ndev));
+    if (p->device < 0 || p->device >= ndev)
+        return fail("device %d not available (%d HIP devices)", p->device, ndev);
+    HIPCK(hipSetDevice(p->device));
+    if (p->d_coef) return 0;
+    HIPCK(hipMalloc(&p->d_coef, p->coef.size() * sizeof(double)));
+    HIPCK(hipMemcpy(p->d_coef, p->coef.data(), p->coef.size() * sizeof(double),
+                    hipMemcpyHostToDevice));
+    HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    return 0;
+}
+
+// ===========================================================================
+// host ray entry: first_point + vacuum_plasma_refraction (src/solve.jl:7-74)
+// ===========================================================================
+static double host_psi(const torj_plasma_s *p, const double x[3]) {
+    return eval_one(p->coef.data(), p->g, std::hypot(x[0], x[1]), x[2], F_PSI);
+}
+
+// IMAS.toroidal_intersection for the grid rectangle (src/solve.jl:22-24):
+// smallest t > 0 at which p0 + t v meets the surface of revolution of the
+// polygon (R_k, Z_k).  Parity unpinned (IMAS not available).
+static double toroidal_intersection(const double *Rp, const double *Zp, int np, const double p0[3],
+                                    const double v[3]) {
+    double best = INFINITY;
+    for (int s = 0; s + 1 < np; s++) {
+        const double Ra = Rp[s], Za = Zp[s], Rb = Rp[s + 1], Zb = Zp[s + 1];
+        if (Zb == Za) {
+            if (v[2] == 0.0) continue;
+            const double t = (Za - p0[2]) / v[2];
+            if (!(t > 0)) continue;
+            const double R = std::hypot(p0[0] + t * v[0], p0[1] + t * v[1]);
+            if (R >= std::min(Ra, Rb) && R <= std::max(Ra, Rb)) best = std::min(best, t);
+            continue;
+        }
+        // R(t)^2 = (al + be t)^2 on the cone through the segment
+        const double k = (Rb - Ra) / (Zb - Za);
+        const double al = Ra + (p0[2] - Za) * k, be = v[2] * k;
+        const double A = v[0] * v[0] + v[1] * v[1] - be * be;
+        const double B = 2.0 * (p0[0] * v[0] + p0[1] * v[1] - al * be);
+        const double C = p0[0] * p0[0] + p0[1] * p0[1] - al * al;
+        double ts[2];
+        int nt = 0;
+        if (std::fabs(A) < 1e-300) {
+            if (B != 0) ts[nt++] = -C / B;
+        } else {
+            const double disc = B * B - 4 * A * C;
+            if (disc >= 0) {
+                const double sq = std::sqrt(disc);
+                ts[nt++] = (-B - sq) / (2 * A);
+                ts[nt++] = (-B + sq) / (2 * A);
+            }
+        }
+        for (int q = 0; q < nt; q++) {
+            const double t = ts[q];
+            if (!(t > 0)) continue;
+            const double sp = (p0[2] + t * v[2] - Za) / (Zb - Za);
+            if (sp < 0 || sp > 1 || al + be * t < 0) continue;
+            best = std::min(best, t);
+        }
+    }
+    return best;
+}
+
+static int host_first_point(const torj_plasma_s *p, const double x0[3], const double N0[3],
+                            double out[3]) {
+    const Grid &g = p->g;
+    double pp[3] = {x0[0], x0[1], x0[2]};
+    const double R0 = std::hypot(x0[0], x0[1]);
+    const bool on_grid = g.R1 <= R0 && R0 <= g.Rn && g.Z1 <= x0[2] && x0[2] <= g.Zn;  // :7-11
+    if (!on_grid) {
+        const double Rp[5] = {g.R1, g.Rn, g.Rn, g.R1, g.R1};
+        const double Zp[5] = {g.Z1, g.Z1, g.Zn, g.Zn, g.Z1};
+        const double t = toroidal_intersection(Rp, Zp, 5, x0, N0);
+        if (!std::isfinite(t)) return ST_ENTRY_FAIL;
+        for (int k = 0; k < 3; k++) pp[k] = x0[k] + N0[k] * t;
+    }
+    auto G = [&](double t) {
+        const double q[3] = {pp[0] + t * N0[0], pp[1] + t * N0[1], pp[2] + t * N0[2]};
+        return host_psi(p, q) - p->psi_prof_max;
+    };
+    // find_zero(g, (0, 0.5), Bisection()) (:29), bisected to machine precision
+    double a = 0.0, b = 0.5, ga = G(a), gb = G(b);
+    if (ga != 0.0 && gb != 0.0) {
+        if ((ga > 0) == (gb > 0)) return ST_ENTRY_FAIL;
+        for (int it = 0; it < 200; it++) {
+            const double m = 0.5 * (a + b);
+            if (m <= a || m >= b) break;
+            const double gm = G(m);
+            if (gm == 0.0) {
+                a = b = m;
+                ga = gb = 0.0;
+                break;
+            }
+            if ((gm > 0) == (ga > 0)) {
+                a = m;
+                ga = gm;
+            } else {
+                b = m;
+                gb = gm;
+            }
+        }
+    }
+    const double t = (std::fabs(ga) <= std::fabs(gb)) ? a : b;
+    for (int k = 0; k < 3; k++) pp[k] += t * N0[k];
+    const double psi_ref = host_psi(p, pp);
+    if (!(std::fabs(psi_ref - p->psi_prof_max) < 1e-6)) return ST_ENTRY_FAIL;  // :32
+    if (psi_ref > p->psi_prof_max)                                              // :33-36
+        for (int k = 0; k < 3; k++) pp[k] += 2.0 * (psi_ref - p->psi_prof_max) * N0[k];
+    for (int k = 0; k < 3; k++) out[k] = pp[k];
+    return ST_OK;
+}
+
+static void host_eval_plasma(const torj_plasma_s *p, const double x[3], const double N[3],
+                             double omega, double &X, double &Y, double &Npar, double b[3]) {
+    PlasmaPoint pt;
+    plasma_point<false>(p->coef.data(), p->g, make_consts(omega), x, pt);
+    X = pt.X;
+    Y = pt.Y;
+    for (int k = 0; k < 3; k++) b[k] = pt.b[k];
+    Npar = N[0] * b[0] + N[1] * b[1] + N[2] * b[2];
+}
+
+// The 3 refraction equations (:40-49) have the root N = n0 + (cos_i -
+// sqrt(q^2 - sin_i^2)) n with q^2 = N_s^2(N.b): solved as a scalar equation in q.
+static int host_refraction(const torj_plasma_s *p, const double pp[3], const double N0[3],
+                           double omega, int mode, double N[3]) {
+    double X, Y, Npar, b[3];
+    host_eval_plasma(p, pp, N0, omega, X, Y, Npar, b);
+    const double Nest = refractive_index_sq(X, Y, 0.0, mode);
+    if (Nest <= 0) return ST_REFLECTED;  // :57-59
+    double q = std::sqrt(Nest);
+    const double R = std::hypot(pp[0], pp[1]);
+    double v, dR, dZ;
+    eval_grad_one(p->coef.data(), p->g, R, pp[2], F_PSI, v, dR, dZ);
+    double n[3] = {dR * pp[0] / R, dR * pp[1] / R, dZ};
+    const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    for (double &c : n) c /= nn;
+    const double n0n = std::sqrt(N0[0] * N0[0] + N0[1] * N0[1] + N0[2] * N0[2]);
+    const double n0[3] = {N0[0] / n0n, N0[1] / n0n, N0[2] / n0n};
+    const double ci = -(n[0] * n0[0] + n[1] * n0[1] + n[2] * n0[2]);
+    const double si2 = 1.0 - ci * ci;
+    const double nb = n[0] * b[0] + n[1] * b[1] + n[2] * b[2];
+    const double n0b = n0[0] * b[0] + n0[1] * b[1] + n0[2] * b[2];
+    auto resid = [&](double qq, bool &ok) {
+        const double rt = qq * qq - si2;
+        ok = rt >= 0;
+        if (!ok) return 0.0;
+        const double np = n0b + (ci - std::sqrt(rt)) * nb;
+        return qq * qq - refractive_index_sq(X, Y, np, mode);
+    };
+    for (int it = 0; it < 100; it++) {
+        bool ok;
+        const double r = resid(q, ok);
+        if (!ok) return ST_REFLECTED;
+        const double h = 1e-7 * q;
+        bool o1, o2;
+        const double dr = (resid(q + h, o1) - resid(q - h, o2)) / (2 * h);
+        if (!o1 || !o2 || !(dr != 0)) return ST_ENTRY_FAIL;
+        const double dq = r / dr;
+        q -= dq;
+        if (std::fabs(dq) <= 1e-16 * q) break;
+    }
+    const double s = std::sqrt(q * q - si2);
+    for (int k = 0; k < 3; k++) N[k] = n0[k] + (ci - s) * n[k];
+    return ST_OK;
+}
+
+// ===========================================================================
+// launch fan (host), src/launch.jl:24-132
+// ===========================================================================
+// FastGaussQuadrature.gausshermite(n): Newton on the orthonormal Hermite
+// recurrence, asymptotic initial guesses, ascending order.
+static void gauss_hermite(int n, std::vector<double> &x, std::vector<double> &w) {
+    x.assign(n, 0.0);
+    w.assign(n, 0.0);
+    const int m = (n + 1) / 2;
+    std::vector<double> xd(n);
+    double z = 0;
+    for (int i = 0; i < m; i++) {
+        if (i == 0)
+            z = std::sqrt(2.0 * n + 1.0) - 1.85575 * std::pow(2.0 * n + 1.0, -1.0 / 6.0);
+        else if (i == 1)
+            z -= 1.14 * std::pow((double)n, 0.426) / z;
+        else if (i == 2)
+            z = 1.86 * z - 0.86 * xd[0];
+        else if (i == 3)
+            z = 1.91 * z - 0.91 * xd[1];
+        else
+            z = 2.0 * z - xd[i - 2];
+        double pp = 1.0;
+        for (int it = 0; it < 200; it++) {
+            double p1 = 0.7511255444649425, p2 = 0.0;  // pi^(-1/4)
+            for (int j = 0; j < n; j++) {
+                const double p3 = p2;
+                p2 = p1;
+                p1 = z * std::sqrt(2.0 / (j + 1)) * p2 - std::sqrt((double)j / (j + 1)) * p3;
+            }
+            pp = std::sqrt(2.0 * n) * p2;
+            const double dz = p1 / pp;
+            z -= dz;
+            if (std::fabs(dz) <= 1e-15 * std::max(1.0, std::fabs(z))) break;
+        }
+        xd[i] = z;
+        x[n - 1 - i] = z;
+        x[i] = -z;
+        w[i] = w[n - 1 - i] = 2.0 / (pp * pp);
+    }
+}
+
+struct Rings {
+    std::vector<double> r, rw;
+    std::vector<int> nth;
+    int total = 0;
+};
+
+static Rings make_rings(int N_rings, int min_az, double w) {
+    Rings R;
+    std::vector<double> x, wt;
+    gauss_hermite(2 * N_rings + 2, x, wt);  // :72
+    for (int i = 0; i < N_rings; i++) {
+        R.r.push_back(x[N_rings + 1 + i] * (w / std::sqrt(2.0)));
+        R.rw.push_back(wt[N_rings + 1 + i] * (w / std::sqrt(2.0)));
+    }
+    for (int i = 0; i < N_rings; i++) {  // :80-83
+        const long k = std::lround(min_az * R.r[i] / R.r[0]);
+        R.nth.push_back(k < 1 ? 1 : (int)k);
+        R.total += R.nth.back();
+    }
+    return R;
+}
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int torj_abi_version(void) { return TORJ_ABI_VERSION; }
+
+const char *torj_last_error(void) { return g_err.c_str(); }
+
+int torj_device_count(int *n) {
+    HIPCK(hipGetDeviceCount(n));
+    return 0;
+}
+
+int torj_abs_al_init(int n) {
+    if (n < 1 || n > kMaxGL) return fail("abs_Al_init: order %d outside [1, %d]", n, kMaxGL);
+    std::lock_guard<std::mutex> lk(g_gl_mu);
+    GLTable t{};
+    t.n = n;
+    gauss_legendre(n, t.t, t.w);
+    for (int i = 0; i < n; i++) t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);
+    g_gl_host = t;
+    g_gl_version++;
+    return 0;
+}
+
+int torj_plasma_create(int nR, int nZ, const double *R, const double *Z, const double *psi_norm,
+                       int n_prof, const double *psi_prof, const double *ne_prof,
+                       const double *Te_prof, const double *Br, const double *Bz,
+                       const double *Bphi, int n_eq, const double *eq_psi, const double *eq_vol,
+                       int device, torj_plasma_t *out) {
+    if (!out) return fail("out is NULL");
+    if (nR < 2 || nZ < 2 || n_prof < 2 || n_eq < 2) return fail("Plasma: grids need >= 2 points");
+    const size_t nd = (size_t)nR * nZ, nc = (size_t)(nR + 2) * (nZ + 2);
+    std::vector<double> cpsi(nc), cne(nc), cte(nc), cbr(nc), cbz(nc), cbp(nc);
+    bspl2d_prefilter(nR, nZ, psi_norm, cpsi.data());
+    bspl2d_prefilter(nR, nZ, Br, cbr.data());
+    bspl2d_prefilter(nR, nZ, Bz, cbz.data());
+    bspl2d_prefilter(nR, nZ, Bphi, cbp.data());
+    // make_2d_prof_spline (src/plasma.jl:16-22)
+    auto prof2d = [&](const double *prof, std::vector<double> &c2) {
+        std::vector<double> pr = uniform_range(psi_prof[0], psi_prof[n_prof - 1], n_prof);
+        std::vector<double> p2(n_prof), c1(n_prof + 2), d2(nd);
+        natcubic(n_prof, psi_prof, prof, n_prof, pr.data(), p2.data());
+        for (double &v : p2) v = std::log(v);
+        bspl1d_prefilter(n_prof, p2.data(), 1, c1.data(), 1);
+        for (size_t k = 0; k < nd; k++)
+            d2[k] = bspl1d_eval(c1, n_prof, psi_prof[0], psi_prof[n_prof - 1], psi_norm[k]);
+        bspl2d_prefilter(nR, nZ, d2.data(), c2.data());
+    };
+    prof2d(ne_prof, cne);
+    prof2d(Te_prof, cte);
+    auto *p = new torj_plasma_s();
+    // volume_psi_spline (src/plasma.jl:42-44)
+    std::vector<double> pr = uniform_range(eq_psi[0], eq_psi[n_eq - 1], n_eq), v2(n_eq);
+    natcubic(n_eq, eq_psi, eq_vol, n_eq, pr.data(), v2.data());
+    p->n_vol = n_eq;
+    p->v1 = eq_psi[0];
+    p->vn = eq_psi[n_eq - 1];
+    p->vol_coef.assign(n_eq + 2, 0.0);
+    bspl1d_prefilter(n_eq, v2.data(), 1, p->vol_coef.data(), 1);
+    p->psi_prof_max = *std::max_element(psi_prof, psi_prof + n_prof);
+    const double *fields[6] = {cpsi.data(), cne.data(), cte.data(), cbr.data(), cbz.data(), cbp.data()};
+    const int rc = plasma_finish(p, nR, nZ, R[0], R[nR - 1], Z[0], Z[nZ - 1], fields, device, out);
+    if (rc) delete p;
+    return rc;
+}
+
+int torj_plasma_create_from_coefs(int nR, int nZ, double R1, double Rn, double Z1, double Zn,
+                                  const double *c_psi, const double *c_lnne, const double *c_lnTe,
+                                  const double *c_Br, const double *c_Bz, const double *c_Bphi,
+                                  int n_vol, double vol_psi1, double vol_psin,
+                                  const double *vol_coefs, double psi_prof_max, int device,
+                                  torj_plasma_t *out) {
+    if (!out) return fail("out is NULL");
+    if (nR < 2 || nZ < 2 || n_vol < 2) return fail("Plasma: grids need >= 2 points");
+    auto *p = new torj_plasma_s();
+    p->n_vol = n_vol;
+    p->v1 = vol_psi1;
+    p->vn = vol_psin;
+    p->vol_coef.assign(vol_coefs, vol_coefs + n_vol + 2);
+    p->psi_prof_max = psi_prof_max;
+    const double *fields[6] = {c_psi, c_lnne, c_lnTe, c_Br, c_Bz, c_Bphi};
+    const int rc = plasma_finish(p, nR, nZ, R1, Rn, Z1, Zn, fields, device, out);
+    if (rc) delete p;
+    return rc;
+}
+
+int torj_plasma_destroy(torj_plasma_t p) {
+    if (!p) return 0;
+    if (p->d_coef) (void)hipSetDevice(p->device);
+    if (p->d_coef) (void)hipFree(p->d_coef);
+    if (p->stream) (void)hipStreamDestroy(p->stream);
+    delete p;
+    return 0;
+}
+
+int torj_plasma_get_coefs(torj_plasma_t p, int field, double *out) {
+    if (!p || field < 0 || field > 5) return fail("bad plasma handle or field index");
+    const size_t nodes = (size_t)(p->g.nR + 2) * (p->g.nZ + 2);
+    for (size_t k = 0; k < nodes; k++) out[k] = p->coef[k * kNF + kFieldSlot[field]];
+    return 0;
+}
+
+double torj_plasma_psi_prof_max(torj_plasma_t p) { return p ? p->psi_prof_max : NAN; }
+
+int torj_plasma_volume(torj_plasma_t p, int n, const double *psi, double *vol) {
+    if (!p) return fail("bad plasma handle");
+    for (int i = 0; i < n; i++) vol[i] = bspl1d_eval(p->vol_coef, p->n_vol, p->v1, p->vn, psi[i]);
+    return 0;
+}
+
+int torj_shell_volumes(torj_plasma_t p, int n_psi, const double *g, double *dV) {
+    if (!p) return fail("bad plasma handle");
+    for (int j = 0; j + 1 < n_psi; j++)
+        dV[j] = bspl1d_eval(p->vol_coef, p->n_vol, p->v1, p->vn, g[j + 1]) -
+                bspl1d_eval(p->vol_coef, p->n_vol, p->v1, p->vn, g[j]);
+    return 0;
+}
+
+void torj_pol_tor_angles_2_vector(double pol, double tor, double N[3]) {
+    // IMAS ec_launchers convention: angle_pol = atan2(-k_Z, -k_R), angle_tor = asin(k_phi / k)
+    N[0] = -std::cos(pol) * std::cos(tor);
+    N[1] = std::sin(tor);
+    N[2] = -std::sin(pol) * std::cos(tor);
+}
+
+int torj_launch_peripheral_rays(const double x0[3], const double N0[3], double w,
+                                double inv_curv, double f, int N_rings, int min_az, int normalize,
+                                int *n_rays, double *pos, double *dir, double *weights) {
+    if (N_rings < 2) return fail("ArgumentError: N_rings = %d < 2 which is the minimum", N_rings);
+    const Rings RG = make_rings(N_rings, min_az, w);
+    if (n_rays) *n_rays = RG.total;
+    if (!pos) return 0;
+    const int n = RG.total;
+    const double nn = std::sqrt(N0[0] * N0[0] + N0[1] * N0[1] + N0[2] * N0[2]);
+    const double n0[3] = {N0[0] / nn, N0[1] / nn, N0[2] / nn};
+    const bool fin = std::isfinite(inv_curv);
+    double w0 = w, xw[3] = {0, 0, 0};
+    if (fin) {  // :34-47 Gaussian-beam waist
+        const double Rc = 1.0 / inv_curv, lam = kC / f;
+        const double w4 = w * w * w * w;
+        w0 = (lam * std::fabs(Rc) * w) / std::sqrt(lam * lam * Rc * Rc + kPi * kPi * w4);
+        const double zw = kPi * kPi * Rc * w4 / (lam * lam * Rc * Rc + kPi * kPi * w4);
+        for (int k = 0; k < 3; k++) xw[k] = x0[k] - n0[k] * zw;
+    }
+    double ec[3] = {1.0, 0.0, -n0[0] / n0[2]};                     // :54-57
+    double eu[3] = {-n0[0] * n0[1] / n0[2], n0[2] - n0[0], -n0[1]};  // :61-64
+    const double nc = std::sqrt(ec[0] * ec[0] + ec[1] * ec[1] + ec[2] * ec[2]);
+    const double nu = std::sqrt(eu[0] * eu[0] + eu[1] * eu[1] + eu[2] * eu[2]);
+    for (int k = 0; k < 3; k++) {
+        ec[k] /= nc;
+        eu[k] /= nu;
+    }
+    const double sg = inv_curv > 0 ? 1.0 : (inv_curv < 0 ? -1.0 : 0.0);
+    int kk = 0;
+    for (int i = 0; i < N_rings; i++) {
+        const int nt = RG.nth[i];
+        for (int j = 0; j < nt; j++) {
+            const double th = 2.0 * kPi * (double)j / (double)nt;
+            const double chi = RG.r[i] * std::cos(th), ups = RG.r[i] * std::sin(th);
+            const int q = kk + j;
+            double P[3], D[3];
+            for (int k = 0; k < 3; k++) P[k] = chi * ec[k] + ups * eu[k] + x0[k];
+            if (fin) {
+                for (int k = 0; k < 3; k++) D[k] = w0 / w * (chi * ec[k] + ups * eu[k]) * sg + xw[k];
+                if (inv_curv < 0.0)
+                    for (int k = 0; k < 3; k++) D[k] -= P[k];
+                else
+                    for (int k = 0; k < 3; k++) D[k] = -D[k] + P[k];
+                const double dn = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
+                for (double &c : D) c /= dn;
+            } else {
+                for (int k = 0; k < 3; k++) D[k] = n0[k];
+            }
+            for (int k = 0; k < 3; k++) {
+                pos[(size_t)k * n + q] = P[k];
+                dir[(size_t)k * n + q] = D[k];
+            }
+            weights[q] = RG.r[i] * RG.rw[i] * (2.0 * kPi / (double)nt);
+        }
+        kk += nt;
+    }
+    if (normalize) {  // :125-129
+        double s = 0;
+        for (int i = 0; i < n; i++) s += weights[i];
+        for (int i = 0; i < n; i++) weights[i] /= s;
+    } else {
+        for (int i = 0; i < n; i++) weights[i] *= 2.0 / (w * w * kPi);
+    }
+    return 0;
+}
+
+int torj_ray_entry(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
+                   int mode, double *xp, double *Np, double *s0, int *status) {
+    if (!p) return fail("bad plasma handle");
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int i = 0; i < n; i++) {
+        const double a[3] = {x0[i], x0[(size_t)n + i], x0[2 * (size_t)n + i]};
+        const double d[3] = {N0[i], N0[(size_t)n + i], N0[2 * (size_t)n + i]};
+        double xo[3] = {NAN, NAN, NAN}, No[3] = {NAN, NAN, NAN};
+        int st = host_first_point(p, a, d, xo);
+        if (st == ST_OK && !(host_psi(p, xo) <= p->psi_prof_max)) st = ST_ENTRY_FAIL;  // :138
+        if (st == ST_OK) st = host_refraction(p, xo, d, omega, mode, No);
+        if (st == ST_OK) {  // :141 |D| < 1e-12
+            double X, Y, Npar, b[3];
+            host_eval_plasma(p, xo, No, omega, X, Y, Npar, b);
+            const double D = No[0] * No[0] + No[1] * No[1] + No[2] * No[2] -
+                             refractive_index_sq(X, Y, Npar, mode);
+            if (!(std::fabs(D) < 1e-12)) st = ST_ENTRY_FAIL;
+        }
+        for (int k = 0; k < 3; k++) {
+            xp[(size_t)k * n + i] = xo[k];
+            Np[(size_t)k * n + i] = No[k];
+        }
+        s0[i] = std::sqrt((xo[0] - a[0]) * (xo[0] - a[0]) + (xo[1] - a[1]) * (xo[1] - a[1]) +
+                          (xo[2] - a[2]) * (xo[2] - a[2]));
+        status[i] = st;
+    }
+    return 0;
+}
+
+}  // extern "C"
+
+// ---- device helpers ----
+template <typename T>
+static int dupload(T **d, const T *h, size_t n, hipStream_t s) {
+    *d = nullptr;
+    if (!h || n == 0) return 0;
+    HIPCK(hipMalloc(d, n * sizeof(T)));
+    HIPCK(hipMemcpyAsync(*d, h, n * sizeof(T), hipMemcpyHostToDevice, s));
+    return 0;
+}
+template <typename T>
+static int dalloc(T **d, size_t n, bool want) {
+    *d = nullptr;
+    if (!want || n == 0) return 0;
+    HIPCK(hipMalloc(d, n * sizeof(T)));
+    return 0;
+}
+template <typename T>
+static int ddownload(T *h, const T *d, size_t n, hipStream_t s) {
+    if (!h || !d || n == 0) return 0;
+    HIPCK(hipMemcpyAsync(h, d, n * sizeof(T), hipMemcpyDeviceToHost, s));
+    return 0;
+}
+
+struct DevBufs {
+    std::vector<void *> ptrs;
+    ~DevBufs() {
+        for (void *q : ptrs)
+            if (q) (void)hipFree(q);
+    }
+    template <typename T>
+    T *track(T *q) {
+        ptrs.push_back((void *)q);
+        return q;
+    }
+};
+
+static inline int nblocks(int n, int b) { return (n + b - 1) / b; }
+
+extern "C" {
+
+int torj_eval_plasma(torj_plasma_t p, int n, const double *x, const double *N, double omega,
+                     double *out) {
+    if (!p) return fail("bad plasma handle");
+    if (n <= 0) return 0;
+    if (ensure_device(p)) return -1;
+    DevBufs B;
+    double *dx, *dN, *dout;
+    if (dupload(&dx, x, 3 * (size_t)n, p->stream) || dupload(&dN, N, 3 * (size_t)n, p->stream) ||
+        dalloc(&dout, 13 * (size_t)n, true))
+        return -1;
+    B.track(dx), B.track(dN), B.track(dout);
+    EvalArgs a{};
+    a.coef = p->d_coef;
+    a.g = p->g;
+    a.k = make_consts(omega);
+    a.omega = omega;
+    a.n = n;
+    a.x = dx;
+    a.N = dN;
+    a.out = dout;
+    hipLaunchKernelGGL(k_eval_plasma, dim3(nblocks(n, 256)), dim3(256), 0, p->stream, a);
+    HIPCK(hipGetLastError());
+    if (ddownload(out, dout, 13 * (size_t)n, p->stream)) return -1;
+    HIPCK(hipStreamSynchronize(p->stream));
+    return 0;
+}
+
+int torj_dispersion(torj_plasma_t p, int n, const double *x, const double *N, double omega,
+                    int mode, double *D, double *du, double *alpha) {
+    if (!p) return fail("bad plasma handle");
+    if (n <= 0) return 0;
+    if (ensure_device(p)) return -1;
+    if (alpha && ensure_gl_on_device(p->device)) return -1;
+    DevBufs B;
+    double *dx, *dN, *dD, *ddu, *dal;
+    if (dupload(&dx, x, 3 * (size_t)n, p->stream) || dupload(&dN, N, 3 * (size_t)n, p->stream) ||
+        dalloc(&dD, n, D != nullptr) || dalloc(&ddu, 6 * (size_t)n, du != nullptr) ||
+        dalloc(&dal, n, alpha != nullptr))
+        return -1;
+    B.track(dx), B.track(dN), B.track(dD), B.track(ddu), B.track(dal);
+    EvalArgs a{};
+    a.coef = p->d_coef;
+    a.g = p->g;
+    a.k = make_consts(omega);
+    a.omega = omega;
+    a.mode = mode;
+    a.n = n;
+    a.x = dx;
+    a.N = dN;
+    a.D = dD;
+    a.du = ddu;
+    a.alpha = dal;
+    if (alpha)
+        hipLaunchKernelGGL(k_dispersion<true>, dim3(nblocks(n, 256)), dim3(256), 0, p->stream, a);
+    else
+        hipLaunchKernelGGL(k_dispersion<false>, dim3(nblocks(n, 256)), dim3(256), 0, p->stream, a);
+    HIPCK(hipGetLastError());
+    if (ddownload(D, dD, n, p->stream) || ddownload(du, ddu, 6 * (size_t)n, p->stream) ||
+        ddownload(alpha, dal, n, p->stream))
+        return -1;
+    HIPCK(hipStreamSynchronize(p->stream));
+    return 0;
+}
+
+static int batched_scalar(bool albajar, int n, const double *omega, const double *X,
+                          const double *Y, const double *Nabs, const double *Npar,
+                          const double *Te, int mode, double *out) {
+    if (n <= 0) return 0;
+    int dev = 0;
+    HIPCK(hipGetDevice(&dev));
+    if (albajar && ensure_gl_on_device(dev)) return -1;
+    DevBufs B;
+    AlbArgs a{};
+    a.n = n;
+    a.mode = mode;
+    double *d[7];
+    const double *h[6] = {omega, X, Y, Nabs, Npar, Te};
+    for (int k = 0; k < 6; k++) {
+        d[k] = nullptr;
+        if (h[k] && dupload(&d[k], h[k], n, nullptr)) return -1;
+        B.track(d[k]);
+    }
+    if (dalloc(&d[6], n, true)) return -1;
+    B.track(d[6]);
+    a.omega = d[0], a.X = d[1], a.Y = d[2], a.Nabs = d[3], a.Npar = d[4], a.Te = d[5];
+    a.out = d[6];
+    if (albajar)
+        hipLaunchKernelGGL(k_albajar, dim3(nblocks(n, 256)), dim3(256), 0, nullptr, a);
+    else
+        hipLaunchKernelGGL(k_refr, dim3(nblocks(n, 256)), dim3(256), 0, nullptr, a);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpy(out, d[6], n * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int torj_abs_albajar_fast(int n, const double *omega, const double *X, const double *Y,
+                          const double *Nabs, const double *Npar, const double *Te, int mode,
+                          double *alpha) {
+    return batched_scalar(true, n, omega, X, Y, Nabs, Npar, Te, mode, alpha);
+}
+
+int torj_refractive_index_sq(int n, const double *X, const double *Y, const double *Npar, int mode,
+                             double *out) {
+    return batched_scalar(false, n, nullptr, X, Y, nullptr, Npar, nullptr, mode, out);
+}
+
+int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                      const double *N0, const double *weights, int n_psi, const double *grid,
+                      double *state, int *status, int *steps, double *dP, double *Pdep,
+                      double *traj, uint64_t *counters, void *stream) {
+    if (!p || !cfg) return fail("bad plasma handle or cfg");
+    if (n <= 0) return 0;
+    if (!x0 || !N0 || !state || !status || !steps) return fail("x0, N0, state, status, steps required");
+    if (cfg->n_steps < 0) return fail("n_steps < 0");
+    if (cfg->mode != 1 && cfg->mode != -1) return fail("mode must be +1 (X) or -1 (O)");
+    if (!(cfg->ds > 0)) return fail("ds must be > 0");
+    const bool depo = n_psi >= 2 && grid && dP;
+    const bool tr = cfg->traj_stride > 0 && traj;
+    if (ensure_device(p)) return -1;
+    if (cfg->absorption && ensure_gl_on_device(p->device)) return -1;
+    hipStream_t s = (hipStream_t)stream;
+    TraceArgs a{};
+    a.coef = p->d_coef;
+    a.g = p->g;
+    a.k = make_consts(cfg->omega);
+    a.omega = cfg->omega;
+    a.mode = cfg->mode;
+    a.ds = cfg->ds;
+    a.n_steps = cfg->n_steps;
+    a.chunk_steps = cfg->chunk_steps;
+    a.psi_exit = cfg->psi_exit;
+    a.P_min = cfg->P_min;
+    a.n = n;
+    a.x0 = x0;
+    a.N0 = N0;
+    a.w = weights;
+    a.state = state;
+    a.status = status;
+    a.steps = steps;
+    a.counters = (unsigned long long *)counters;
+    if (depo) {
+        // host copy of the grid is not available here (device pointer): the
+        // uniform flag / spacing come from a small D2H read of the endpoints
+        double ends[2];
+        HIPCK(hipMemcpyAsync(&ends[0], grid, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCK(hipMemcpyAsync(&ends[1], grid + n_psi - 1, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        a.n_psi = n_psi;
+        a.grid = grid;
+        a.g0 = ends[0];
+        a.ginv = (n_psi - 1) / (ends[1] - ends[0]);
+        a.grid_uniform = std::isfinite(a.ginv) && a.ginv > 0;  // index is corrected on the grid
+        a.dP = dP;
+        a.Pdep = Pdep;
+    }
+    if (tr) {
+        a.traj_stride = cfg->traj_stride;
+        a.n_save = cfg->n_steps / cfg->traj_stride;
+        a.traj = traj;
+        if (a.n_save > 0)
+            HIPCK(hipMemsetAsync(traj, 0xFF, (size_t)a.n_save * 4 * n * sizeof(double), s));  // NaN
+    }
+    const dim3 grd(nblocks(n, 256)), blk(256);
+#define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
+    if (cfg->absorption) {
+        if (depo) {
+            if (tr) LAUNCH(true, true, true); else LAUNCH(true, true, false);
+        } else {
+            if (tr) LAUNCH(true, false, true); else LAUNCH(true, false, false);
+        }
+    } else {
+        if (depo) {
+            if (tr) LAUNCH(false, true, true); else LAUNCH(false, true, false);
+        } else {
+            if (tr) LAUNCH(false, false, true); else LAUNCH(false, false, false);
+        }
+    }
+#undef LAUNCH
+    HIPCK(hipGetLastError());
+    return 0;
+}
+
+int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+               const double *N0, const double *weights, int n_psi, const double *grid,
+               double *state, int *status, int *steps, double *dP, double *Pdep, double *traj) {
+    if (!p || !cfg) return fail("bad plasma handle or cfg");
+    if (n <= 0) return 0;
+    if (ensure_device(p)) return -1;
+    hipStream_t s = p->stream;
+    const bool depo = n_psi >= 2 && grid;
+    const int n_save = cfg->traj_stride > 0 ? cfg->n_steps / cfg->traj_stride : 0;
+    DevBufs B;
+    double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dstate, *ddP = nullptr, *dPdep = nullptr,
+                                *dtraj = nullptr;
+    int *dstatus, *dsteps;
+    if (dupload(&dx0, x0, 3 * (size_t)n, s) || dupload(&dN0, N0, 3 * (size_t)n, s)) return -1;
+    B.track(dx0), B.track(dN0);
+    if (weights) {
+        if (dupload(&dw, weights, n, s)) return -1;
+        B.track(dw);
+    }
+    if (depo) {
+        if (dupload(&dgrid, grid, n_psi, s) || dalloc(&ddP, n_psi + 1, true) ||
+            dalloc(&dPdep, n, true))
+            return -1;
+        B.track(dgrid), B.track(ddP), B.track(dPdep);
+        HIPCK(hipMemsetAsync(ddP, 0, (n_psi + 1) * sizeof(double), s));
+    }
+    if (dalloc(&dstate, 7 * (size_t)n, true) || dalloc(&dstatus, n, true) ||
+        dalloc(&dsteps, n, true))
+        return -1;
+    B.track(dstate), B.track(dstatus), B.track(dsteps);
+    if (traj && n_save > 0) {
+        if (dalloc(&dtraj, (size_t)n_save * 4 * n, true)) return -1;
+        B.track(dtraj);
+    }
+    if (torj_trace_device(p, cfg, n, dx0, dN0, dw, depo ? n_psi : 0, dgrid, dstate, dstatus, dsteps,
+                          ddP, dPdep, dtraj, nullptr, s))
+        return -1;
+    if (ddownload(state, dstate, 7 * (size_t)n, s) || ddownload(status, dstatus, n, s) ||
+        ddownload(steps, dsteps, n, s))
+        return -1;
+    if (depo) {
+        if (ddownload(dP, ddP, n_psi + 1, s) || ddownload(Pdep, dPdep, n, s)) return -1;
+    } else {
+        if (dP) std::fill(dP, dP + (n_psi > 0 ? n_psi + 1 : 1), 0.0);
+        if (Pdep) std::fill(Pdep, Pdep + n, 0.0);
+    }
+    if (traj && n_save > 0 && ddownload(traj, dtraj, (size_t)n_save * 4 * n, s)) return -1;
+    HIPCK(hipStreamSynchronize(s));
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,506 @@
+// torj_math.hpp -- ray-physics math shared by the HIP kernels (device) and the
+// host-side setup code (ray entry, Plasma construction) of libtorj_hip.
+//
+// MI355X design notes:
+//  * All six 2-D B-spline fields live on ONE (R,Z) grid (src/plasma.jl:30-58), so
+//    the 16 basis weights (+ R/Z derivative weights) are computed once per point
+//    and applied to every field.  Coefficients are stored node-interleaved
+//    (8 doubles = 64 B per node: Br, Bphi, Bz, ln ne, ln Te, psi, pad, pad) so a
+//    4x4 stencil is 4 runs of 256 contiguous bytes.
+//  * ForwardDiff's two gradients of the dispersion relation (src/solve.jl:89-90)
+//    are replaced by ONE analytic evaluation of D, dD/dx and dD/dN (the spline
+//    work is shared instead of being redone per dual pass).
+//  * The Albajar Bessel factors J_{m-1}, J_m, J_{m+1} come from two Horner power
+//    series (J_m, J_{m+1}) and the stable downward recurrence for J_{m-1}.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define TORJ_HD __host__ __device__ __forceinline__
+
+namespace torj {
+
+// src/constants.jl:13-26
+constexpr double kC = 2.99792458e8;
+constexpr double kE = 1.602176634e-19;
+constexpr double kMe = 9.1093837015e-31;
+constexpr double kEps0 = 8.8541878128e-12;
+constexpr double kPi = 3.14159265358979323846;
+
+constexpr int kNF = 8;  // doubles per coefficient node
+enum Field { F_BR = 0, F_BPHI = 1, F_BZ = 2, F_LNNE = 3, F_LNTE = 4, F_PSI = 5 };
+
+// ray status codes (include/torj_hip.h)
+enum Status { ST_OK = 0, ST_LEFT_PLASMA = 1, ST_ABSORBED = 2, ST_NAN = 3, ST_REFLECTED = 4,
+              ST_ENTRY_FAIL = 5 };
+
+struct Grid {
+    int nR, nZ;          // data points (coefficients are (nR+2) x (nZ+2))
+    double R1, Z1, Rn, Zn;
+    double hR, hZ, invhR, invhZ;
+};
+
+// value_weights / gradient_weights of Interpolations.jl's Cubic B-spline
+TORJ_HD void bweights(double d, double w[4], double dw[4]) {
+    const double p = 1.0 - d;
+    const double d2 = d * d, p2 = p * p;
+    w[0] = p2 * p * (1.0 / 6.0);
+    w[1] = 2.0 / 3.0 - d2 + 0.5 * d2 * d;
+    w[2] = 2.0 / 3.0 - p2 + 0.5 * p2 * p;
+    w[3] = d2 * d * (1.0 / 6.0);
+    dw[0] = -0.5 * p2;
+    dw[1] = -2.0 * d + 1.5 * d2;
+    dw[2] = 2.0 * p - 1.5 * p2;
+    dw[3] = 0.5 * d2;
+}
+
+TORJ_HD double clampd(double x, double lo, double hi) { return x > hi ? hi : (x < lo ? lo : x); }
+
+// Stencil position on one axis: clamped coordinate, cell index, weights.
+struct Axis {
+    int i;
+    double delta;  // x - clamp(x): Line() extrapolation distance
+    double w[4], dw[4];
+};
+
+TORJ_HD void axis_setup(double x, double x1, double xn, double invh, int n, Axis &a) {
+    const double xc = clampd(x, x1, xn);
+    a.delta = x - xc;
+    const double u = (xc - x1) * invh;
+    int i = (int)floor(u);
+    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+    bweights(u - (double)i, a.w, a.dw);
+    a.i = i;
+}
+
+// Field values with physical R and Z derivatives, Line() extrapolation applied
+// with exactly the derivative ForwardDiff sees through Interpolations'
+// extrapolate(): inside an axis the gradient of the other axis' extension term
+// contributes (mixed derivative), outside it the slope is constant.
+template <int NGRAD, int NVAL>
+struct FieldPack {
+    static constexpr int NG1 = NGRAD > 0 ? NGRAD : 1;
+    double v[NGRAD + NVAL];
+    double dR[NG1], dZ[NG1];
+};
+
+// Evaluate fields [0, NGRAD) with gradients and [NGRAD, NGRAD+NVAL) value-only.
+// `fidx` maps pack slot -> coefficient field index.
+template <int NGRAD, int NVAL>
+TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double R, double Z,
+                         const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
+    constexpr int NT = NGRAD + NVAL;
+    Axis aR, aZ;
+    axis_setup(R, g.R1, g.Rn, g.invhR, g.nR, aR);
+    axis_setup(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
+    const int mR = g.nR + 2;
+    // tensor-product sums accumulated row by row (few live registers):
+    //   v = sum wZ wR c, gr = sum wZ dwR c, gz = sum dwZ wR c, grz = sum dwZ dwR c
+    double v[NT], gr[NT], gz[NT], grz[NT];
+#pragma unroll
+    for (int f = 0; f < NT; f++) v[f] = gr[f] = gz[f] = grz[f] = 0.0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const double *row = coef + ((size_t)(aZ.i + b) * mR + aR.i) * kNF;
+#pragma unroll
+        for (int f = 0; f < NT; f++) {
+            double sv = 0.0, sd = 0.0;
+#pragma unroll
+            for (int a = 0; a < 4; a++) {
+                const double c = row[a * kNF + fidx[f]];
+                sv = fma(aR.w[a], c, sv);
+                sd = fma(aR.dw[a], c, sd);
+            }
+            v[f] = fma(aZ.w[b], sv, v[f]);
+            gz[f] = fma(aZ.dw[b], sv, gz[f]);
+            gr[f] = fma(aZ.w[b], sd, gr[f]);
+            if (f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
+        }
+#ifdef __HIP_DEVICE_COMPILE__
+        // one stencil row in flight at a time: bounds the VGPRs held by
+        // coefficient loads (the step is VALU-bound, not load-latency-bound)
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+    const bool outR = aR.delta != 0.0, outZ = aZ.delta != 0.0;
+#pragma unroll
+    for (int f = 0; f < NT; f++) {
+        const double gR = gr[f] * g.invhR, gZ = gz[f] * g.invhZ;
+        out.v[f] = v[f] + aR.delta * gR + aZ.delta * gZ;
+        if (f < NGRAD) {
+            const int q = f < NGRAD ? f : 0;
+            const double gRZ = grz[f] * (g.invhR * g.invhZ);
+            out.dR[q] = outR ? gR : gR + aZ.delta * gRZ;
+            out.dZ[q] = outZ ? gZ : gZ + aR.delta * gRZ;
+        }
+    }
+}
+
+// single value (e.g. psi for termination / deposition)
+TORJ_HD double eval_one(const double *__restrict__ coef, const Grid &g, double R, double Z, int field) {
+    FieldPack<0, 1> p;
+    const int idx[1] = {field};
+    eval_fields<0, 1>(coef, g, R, Z, idx, p);
+    return p.v[0];
+}
+
+// value + gradient of one field (psi gradient for the flux-surface normal,
+// src/solve.jl:63)
+TORJ_HD void eval_grad_one(const double *__restrict__ coef, const Grid &g, double R, double Z,
+                           int field, double &v, double &dR, double &dZ) {
+    FieldPack<1, 0> p;
+    const int idx[1] = {field};
+    // the reference calls gradient() on the extrapolated object at the point:
+    // Interpolations evaluates the gradient at the clamped position.
+    eval_fields<1, 0>(coef, g, clampd(R, g.R1, g.Rn), clampd(Z, g.Z1, g.Zn), idx, p);
+    v = eval_one(coef, g, R, Z, field);
+    dR = p.dR[0];
+    dZ = p.dZ[0];
+}
+
+// ---------------------------------------------------------------------------
+// dispersion: src/dispersion.jl:21-32 and its analytic partials
+// ---------------------------------------------------------------------------
+TORJ_HD double refractive_index_sq(double X, double Y, double Npar, int mode) {
+    const double Np2 = Npar * Npar, Y2 = Y * Y;
+    const double om = 1.0 - Np2;
+    const double Delta = om * om + 4.0 * Np2 * (1.0 - X) / Y2;
+    return 1.0 - X + (1.0 + (double)mode * sqrt(Delta) + Np2) / (2.0 * (-1.0 + X + Y2)) * X * Y2;
+}
+
+struct NsPartials {
+    double Ns2, dX, dY, dNp;
+};
+
+TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar, int mode) {
+    const double md = (double)mode;
+    const double Np2 = Npar * Npar, Y2 = Y * Y, invY2 = 1.0 / Y2;
+    const double om = 1.0 - Np2, omX = 1.0 - X;
+    const double Delta = om * om + 4.0 * Np2 * omX * invY2;
+    const double sq = sqrt(Delta);
+    const double A = 1.0 + md * sq + Np2;
+    const double Q = 2.0 * (-1.0 + X + Y2);
+    const double invQ = 1.0 / Q;
+    const double G = X * Y2 * invQ;
+    const double dDel_dX = -4.0 * Np2 * invY2;
+    const double dDel_dY = -8.0 * Np2 * omX * invY2 / Y;
+    const double dDel_dNp = -4.0 * Npar * om + 8.0 * Npar * omX * invY2;
+    const double h = md * 0.5 / sq;
+    const double dA_dX = h * dDel_dX, dA_dY = h * dDel_dY, dA_dNp = h * dDel_dNp + 2.0 * Npar;
+    const double invQ2 = invQ * invQ;
+    const double dG_dX = 2.0 * Y2 * (Y2 - 1.0) * invQ2;
+    const double dG_dY = 4.0 * X * Y * (X - 1.0) * invQ2;
+    NsPartials r;
+    r.Ns2 = 1.0 - X + A * G;
+    r.dX = -1.0 + dA_dX * G + A * dG_dX;
+    r.dY = dA_dY * G + A * dG_dY;
+    r.dNp = dA_dNp * G;
+    return r;
+}
+
+// Plasma parameters at a point, with Cartesian gradients (eval_plasma,
+// src/dispersion.jl:7-15; B_spline/n_e/T_e, src/plasma.jl:73-89).
+struct PlasmaPoint {
+    double X, Y, b[3], Babs, B[3], ne;
+    double lnTe, psi;
+    // gradients wrt x (Cartesian)
+    double dX[3], dY[3];
+    double dB[3][3];  // dB[k][c] = dB_c / dx_k
+};
+
+struct Consts {
+    double Cx;  // X = ne * Cx
+    double Cy;  // Y = |B| * Cy
+};
+
+TORJ_HD Consts make_consts(double omega) {
+    Consts c;
+    c.Cx = kE * kE / (kEps0 * kMe * omega * omega);
+    c.Cy = kE / (kMe * omega);
+    return c;
+}
+
+// fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te
+template <bool WITH_TE>
+TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const Consts &k,
+                          const double x[3], PlasmaPoint &p) {
+    const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
+    const double invR = 1.0 / R;
+    const double c = x[0] * invR, s = x[1] * invR;
+    constexpr int NV = WITH_TE ? 1 : 0;
+    FieldPack<4, NV> f;
+    if constexpr (WITH_TE) {
+        const int idx[5] = {F_BR, F_BPHI, F_BZ, F_LNNE, F_LNTE};
+        eval_fields<4, 1>(coef, g, R, x[2], idx, f);
+        p.lnTe = f.v[4];
+    } else {
+        const int idx[4] = {F_BR, F_BPHI, F_BZ, F_LNNE};
+        eval_fields<4, 0>(coef, g, R, x[2], idx, f);
+        p.lnTe = 0.0;
+    }
+    const double Br = f.v[0], Bp = f.v[1], Bz = f.v[2];
+    const double Bx = Br * c - Bp * s, By = Br * s + Bp * c;
+    const double BxR = f.dR[0] * c - f.dR[1] * s, ByR = f.dR[0] * s + f.dR[1] * c;
+    // d/dx, d/dy, d/dz of (Bx, By, Bz): rotation of the cylindrical components
+    p.dB[0][0] = BxR * c + s * By * invR;
+    p.dB[0][1] = ByR * c - s * Bx * invR;
+    p.dB[0][2] = f.dR[2] * c;
+    p.dB[1][0] = BxR * s - c * By * invR;
+    p.dB[1][1] = ByR * s + c * Bx * invR;
+    p.dB[1][2] = f.dR[2] * s;
+    p.dB[2][0] = f.dZ[0] * c - f.dZ[1] * s;
+    p.dB[2][1] = f.dZ[0] * s + f.dZ[1] * c;
+    p.dB[2][2] = f.dZ[2];
+    p.B[0] = Bx;
+    p.B[1] = By;
+    p.B[2] = Bz;
+    const double Babs = sqrt(Bx * Bx + By * By + Bz * Bz);
+    const double invB = 1.0 / Babs;
+    p.Babs = Babs;
+    p.b[0] = Bx * invB;
+    p.b[1] = By * invB;
+    p.b[2] = Bz * invB;
+    const double ne = exp(f.v[3]);
+    p.ne = ne;
+    p.X = ne * k.Cx;
+    p.Y = Babs * k.Cy;
+    const double dlnne[3] = {f.dR[3] * c, f.dR[3] * s, f.dZ[3]};
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        p.dX[q] = p.X * dlnne[q];
+        p.dY[q] = k.Cy * (p.b[0] * p.dB[q][0] + p.b[1] * p.dB[q][1] + p.b[2] * p.dB[q][2]);
+    }
+}
+
+// D(x,N) and its gradients (replaces ForwardDiff in gradΛ!, src/solve.jl:85-93).
+// du = (dD/dN, -dD/dx) / |dD/dN|.
+TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode, double du[6],
+                               double *Npar_out) {
+    const double Npar = N[0] * p.b[0] + N[1] * p.b[1] + N[2] * p.b[2];
+    const NsPartials ns = refractive_index_sq_partials(p.X, p.Y, Npar, mode);
+    const double N2 = N[0] * N[0] + N[1] * N[1] + N[2] * N[2];
+    double dDdN[3], dDdx[3];
+#pragma unroll
+    for (int q = 0; q < 3; q++) dDdN[q] = 2.0 * N[q] - ns.dNp * p.b[q];
+    const double invB = 1.0 / p.Babs;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const double NdB = N[0] * p.dB[q][0] + N[1] * p.dB[q][1] + N[2] * p.dB[q][2];
+        const double bdB = p.b[0] * p.dB[q][0] + p.b[1] * p.dB[q][1] + p.b[2] * p.dB[q][2];
+        const double dNpar = (NdB - Npar * bdB) * invB;
+        dDdx[q] = -(ns.dX * p.dX[q] + ns.dY * p.dY[q] + ns.dNp * dNpar);
+    }
+    const double nrm = sqrt(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
+    const double inv = 1.0 / nrm;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        du[q] = dDdN[q] * inv;
+        du[3 + q] = -dDdx[q] * inv;
+    }
+    if (Npar_out) *Npar_out = Npar;
+    return N2 - ns.Ns2;
+}
+
+// ---------------------------------------------------------------------------
+// Albajar absorption, src/absorption.jl:10-64, 132-226
+// ---------------------------------------------------------------------------
+constexpr int kMaxGL = 64;
+constexpr int kSeriesFast = 15;   // Horner terms, exact to < 1e-17 rel. for arg <= 4
+constexpr int kSeriesSlow = 44;   // arg <= 12
+constexpr double kArgFast = 4.0;
+constexpr double kArgSlow = 12.0;
+
+constexpr double inv_fact(int k) {
+    double f = 1.0;
+    for (int i = 2; i <= k; i++) f *= (double)i;
+    return 1.0 / f;
+}
+// c_nu[k] = 1/(k! (k+nu)!) : S_nu(z) = sum_k c_nu[k] z^k, J_nu(x) = (x/2)^nu S_nu(-x^2/4)
+constexpr double series_coef(int nu, int k) { return inv_fact(k) * inv_fact(k + nu); }
+
+struct GLTable {
+    int n;
+    double t[kMaxGL], w[kMaxGL], st[kMaxGL];  // nodes, weights, sqrt(1-t^2)
+};
+
+// Horner evaluation of S_nu and S_{nu+1} at z; K terms.  Coefficient table
+// kSeries[nu-2][k] (nu = 2..4) lives in constant memory on the device (uniform
+// scalar loads) instead of being materialised as 64-bit immediates.
+constexpr int kSeriesMax = 44;
+struct SeriesTable {
+    double c[3][kSeriesMax];
+};
+constexpr SeriesTable make_series_table() {
+    SeriesTable t{};
+    for (int nu = 2; nu <= 4; nu++)
+        for (int k = 0; k < kSeriesMax; k++) t.c[nu - 2][k] = series_coef(nu, k);
+    return t;
+}
+#ifdef __HIP_DEVICE_COMPILE__
+__constant__ constexpr SeriesTable kSeriesTab = make_series_table();
+#else
+constexpr SeriesTable kSeriesTab = make_series_table();
+#endif
+
+template <int K, int NU>
+TORJ_HD void series_pair(double z, double &Sa, double &Sb) {
+    const double *ca = kSeriesTab.c[NU - 2], *cb = kSeriesTab.c[NU - 1];
+    double a = ca[K - 1], b = cb[K - 1];
+#pragma unroll 7
+    for (int k = K - 2; k >= 0; k--) {
+        a = fma(a, z, ca[k]);
+        b = fma(b, z, cb[k]);
+    }
+    Sa = a;
+    Sb = b;
+}
+
+template <int NU>
+TORJ_HD void series_pair_any(double arg, double z, double &Sa, double &Sb) {
+    // arg = x_m sqrt(1-t^2) < m for |N| <= 1 (x_m < m N_perp / sqrt(1-N_par^2)),
+    // so the 15-term branch is the only one taken on physical rays; the
+    // 44-term branch keeps full accuracy up to arg ~ 12 (no function calls:
+    // a call in the node loop would force the whole RK4 state through the
+    // call ABI / scratch).
+    if (arg <= kArgFast) {
+        series_pair<kSeriesFast, NU>(z, Sa, Sb);
+    } else {
+        series_pair<kSeriesSlow, NU>(z, Sa, Sb);
+    }
+}
+
+struct AlbajarWork {
+    uint32_t n_active;  // calls that reached the harmonic loop
+    uint32_t n_harm;    // harmonic integrals evaluated
+};
+
+// Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
+// abs_Al_pol_fact), returned WITHOUT the Maxwellian normalisation a*(mu/2pi)^1.5
+template <int M>
+TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
+                                double inv_sqNp, double sqNp, double N_perp, double omega_bar,
+                                double Axz, double ea, double e3) {
+    constexpr double md = (double)M;
+    const double r2m1 = r * r - 1.0;
+    const double sq_r = sqrt(r2m1);
+    const double x_m = N_perp * omega_bar * sq_r;
+    const double q = x_m / (md * sqNp);
+    const double K0 = Axz * Axz + ea * ea;
+    const double K1 = Axz * ea * x_m / md;
+    const double K2 = 4.0 * ea * ea / (md * md);
+    const double K3 = q * q * e3 * e3;
+    const double K4 = 2.0 * q * Axz * e3;
+    const double K5 = q * ea * e3 * x_m / md;
+    const double upa0 = inv_sqNp * r * Npar, upa1 = inv_sqNp * sq_r;
+    double sum = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < gl.n; i++) {
+        const double t = gl.t[i], st = gl.st[i];
+        const double arg = x_m * st;
+        const double h = 0.5 * arg;
+        const double h2 = h * h;
+        double Sm, Sm1;
+        series_pair_any<M>(arg, -h2, Sm, Sm1);
+        const double Sl = md * Sm - h2 * Sm1;  // S_{m-1} = m S_m + z S_{m+1}
+        // h^(2m-1)
+        double p = h;
+#pragma unroll
+        for (int k = 1; k < 2 * M - 1; k++) p *= h;
+        const double Jn2 = Sm * Sm;
+        const double bracket =
+            h * (Jn2 * fma(t, fma(K3, t, K4), K0) - K2 * h2 * Sl * Sm1) +
+            st * Sm * (Sl - h2 * Sm1) * fma(K5, t, K1);
+        const double pol = p * bracket;
+        const double u_par = fma(upa1, t, upa0);
+        const double u_perp_sq = r2m1 * (1.0 - t * t);
+        const double gamma = sqrt(1.0 + u_par * u_par + u_perp_sq);
+        sum = fma(gl.w[i] * pol, exp(mu * (1.0 - gamma)), sum);
+    }
+    const double Pm = md / (N_perp * omega_bar);
+    return -mu * Pm * Pm * sum * sq_r;
+}
+
+// abs_Albajar_fast (src/absorption.jl:191-226)
+TORJ_HD double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
+                                double N_par, double Te, int mode, AlbajarWork *work) {
+    if (Te < 20.0) return 0.0;
+    const double mu = kMe * kC * kC / (kE * Te);
+    const double omega_bar = 1.0 / Y;
+    const double cos_t = N_par / N_abs;
+    const double sin_t = sin(acos(cos_t));
+    const double N_perp = sqrt(N_abs * N_abs - N_par * N_par);
+    // abs_Al_N_with_pol_vec (src/absorption.jl:10-64), real form:
+    // e = (e1, i*ea, e3) with e1, ea, e3 real.
+    if (X >= 1.0) return 0.0;
+    const double s2 = sin_t * sin_t, c2 = cos_t * cos_t, omX = 1.0 - X;
+    double rho = Y * Y * (s2 * s2) + 4.0 * omX * omX * c2;
+    if (rho < 0.0) return 0.0;
+    rho = sqrt(rho);
+    const double f = (2.0 * omX) / (2.0 * omX - Y * Y * s2 - (double)mode * Y * rho);
+    double Nt = 1.0 - X * f;
+    if (Nt < 0.0) return 0.0;
+    Nt = sqrt(Nt);
+    if (!(Nt > 0.0) || Nt > 1.0) return 0.0;  // isnan || <= 0 || > 1
+    const double g = 1.0 - (1.0 - Y * Y) * f;
+    double e1 = 0.0, ea = 0.0, e3 = 0.0;
+    if (c2 < 1e-5 || 1.0 - s2 < 1e-5) {
+        if (mode > 0) {
+            ea = sqrt(1.0 / Nt);
+            e1 = -(1.0 / Y * g) * ea;
+        } else {
+            e3 = sqrt(1.0 / Nt);
+        }
+    } else {
+        const double den = omX - Nt * Nt * s2;
+        const double ta = 1.0 + ((omX * Nt * Nt * c2) / (den * den)) * 1.0 / (Y * Y) * (g * g);
+        const double tb = 1.0 + (omX / den) * 1.0 / (Y * Y) * (g * g);
+        const double a_sq = s2 * (ta * ta), b_sq = c2 * (tb * tb);
+        ea = sqrt(1.0 / (Nt * sqrt(a_sq + b_sq)));
+        if (mode <= 0) ea = -ea;
+        e1 = -(1.0 / Y * g) * ea;
+        e3 = -((Nt * Nt * sin_t * cos_t) / den) * e1;
+    }
+    const double sqNp = sqrt(1.0 - N_par * N_par);
+    const double m_0 = sqNp * omega_bar;
+    const double inv_sqNp = 1.0 / sqNp;
+    const double N_eff = (N_perp * N_par) / (1.0 - N_par * N_par);
+    const double Axz = e1 + N_eff * e3;
+    if (work) work->n_active++;
+    double c_abs = 0.0;
+    if (!(2.0 < m_0)) {
+        c_abs += albajar_harmonic<2>(gl, mu, 2.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
+                                     Axz, ea, e3);
+        if (work) work->n_harm++;
+    }
+    if (!(3.0 < m_0)) {  // src/absorption.jl:214 `if m < m_0 continue` (NaN m_0 -> NaN, as reference)
+        c_abs += albajar_harmonic<3>(gl, mu, 3.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
+                                     Axz, ea, e3);
+        if (work) work->n_harm++;
+    }
+    const double a = 1.0 / (1.0 + 105.0 / (128.0 * mu * mu) + 15.0 / (8.0 * mu));
+    const double sm = sqrt(mu / (2.0 * kPi));
+    c_abs *= a * (sm * sm * sm);
+    c_abs = -(c_abs * 2.0 * kPi * kPi / m_0);
+    return c_abs * X * omega / (Y * kC);
+}
+
+// one RHS evaluation of sys! (src/solve.jl:112-114 -> gradΛ!, :85-95)
+template <bool ABS>
+TORJ_HD void ray_rhs(const double *__restrict__ coef, const Grid &g, const Consts &k,
+                     const GLTable &gl, double omega, int mode, const double x[3], const double N[3],
+                     double du[6], double &alpha, AlbajarWork *work) {
+    PlasmaPoint p;
+    plasma_point<ABS>(coef, g, k, x, p);
+    double Npar;
+    dispersion_grad(p, N, mode, du, &Npar);
+    if constexpr (ABS) {
+        const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
+    } else {
+        alpha = 0.0;
+    }
+}
+
+}  // namespace torj

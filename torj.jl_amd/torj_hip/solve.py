@@ -1,0 +1,135 @@
+"""make_ray / make_beam (src/solve.jl) on top of the HIP ray-stepping kernel.
+
+Integration semantics (DESIGN.md "Integrator"): fixed-step RK4 with
+ds = 1e-4 m (the reference's dtmax, src/solve.jl:157), optical depth tau with
+P = exp(-tau), termination checks (psi > 1, P < 1e-6) at the boundaries of the
+reference's 100 chunks (src/solve.jl:145,174,176), and psi-shell deposition
+binned in-kernel.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import numpy as np
+
+from ._lib import TraceCfg, TorjError, check, dptr, f64, iptr, lib, soa
+from .launch import launch_peripheral_rays, pol_tor_angles_2_vector
+
+OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL = range(6)
+STATUS_NAMES = ("OK", "LEFT_PLASMA", "ABSORBED", "NAN", "REFLECTED", "ENTRY_FAIL")
+
+
+class RayEntryError(AssertionError):
+    """The reference's @assert failures in first_point/make_ray (src/solve.jl:32,138,141)
+    and its unhandled reflection return (src/solve.jl:57-59)."""
+
+
+def ray_entry(plasma, x0, N0, omega: float, mode: int):
+    """first_point + vacuum_plasma_refraction for a batch (src/solve.jl:7-74).
+    Returns (x_plasma (n,3), N_plasma (n,3), s0 (n,), status (n,))."""
+    xs, Ns = soa(x0), soa(N0)
+    n = xs.shape[1]
+    xp, Np = np.zeros((3, n)), np.zeros((3, n))
+    s0 = np.zeros(n)
+    st = np.zeros(n, dtype=np.int32)
+    check(lib().torj_ray_entry(plasma.handle, n, dptr(xs), dptr(Ns), float(omega), int(mode),
+                               dptr(xp), dptr(Np), dptr(s0), iptr(st)))
+    return xp.T.copy(), Np.T.copy(), s0, st
+
+
+@dataclass
+class TraceResult:
+    state: np.ndarray     # (n, 7): x, y, z, Nx, Ny, Nz, tau
+    status: np.ndarray    # (n,)
+    steps: np.ndarray     # (n,)
+    dP_shell: np.ndarray  # (n_psi + 1,): sum_rays w * dP per shell, [n_psi] = sum w * P_dep
+    P_dep: np.ndarray     # (n,)
+    traj: np.ndarray | None  # (n, n_save, 4): x, y, z, tau
+
+    @property
+    def P_end(self):
+        return np.exp(-self.state[:, 6])
+
+
+def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps: int,
+          chunk_steps: int | None = None, psi_exit: float = 1.0, P_min: float = 1e-6,
+          absorption: bool = True, psi_grid=None, weights=None, traj_stride: int = 0) -> TraceResult:
+    """Integrate rays from in-plasma start states (x0, N0: (n, 3)) on the GPU."""
+    xs, Ns = soa(x0), soa(N0)
+    n = xs.shape[1]
+    if chunk_steps is None:
+        chunk_steps = max(1, n_steps // 100)
+    cfg = TraceCfg(float(omega), int(mode), float(ds), int(n_steps), int(chunk_steps),
+                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride))
+    g = f64(psi_grid) if psi_grid is not None else np.zeros(0)
+    n_psi = len(g)
+    w = f64(weights) if weights is not None else None
+    state = np.zeros((7, n))
+    status = np.zeros(n, dtype=np.int32)
+    steps = np.zeros(n, dtype=np.int32)
+    dP = np.zeros(n_psi + 1)
+    Pdep = np.zeros(n)
+    n_save = n_steps // traj_stride if traj_stride > 0 else 0
+    traj = np.zeros((n_save, 4, n)) if n_save > 0 else None
+    check(lib().torj_trace(plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi,
+                           dptr(g) if n_psi else None, dptr(state), iptr(status), iptr(steps),
+                           dptr(dP), dptr(Pdep), dptr(traj)))
+    return TraceResult(state.T.copy(), status, steps, dP, Pdep,
+                       traj.transpose(2, 0, 1).copy() if traj is not None else None)
+
+
+def _steps_for(s_max: float, ds: float) -> int:
+    return max(1, int(round(s_max / ds)))
+
+
+def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV, *,
+             ds: float = 1e-4):
+    """make_ray (src/solve.jl:135-181) -> (s, u, P_beam, dP_dV_ray, deposited_power)."""
+    omega = 2.0 * np.pi * f
+    x0 = f64(x0)
+    xp, Np, s0, st = ray_entry(plasma, x0[None], f64(N_vacuum)[None], omega, mode)
+    if st[0] != OK:
+        raise RayEntryError(f"ray entry failed: {STATUS_NAMES[st[0]]}")
+    n_steps = _steps_for(s_max, ds)
+    g = f64(psi_dP_dV)
+    r = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, traj_stride=1)
+    k = int(r.steps[0])
+    s = np.concatenate([[0.0, s0[0]], s0[0] + ds * np.arange(1, k + 1)])
+    u = np.vstack([x0[None], xp, r.traj[0, :k, :3]])
+    P_beam = np.concatenate([[1.0, 1.0], np.exp(-r.traj[0, :k, 3])])
+    dV = plasma.shell_volumes(g)
+    dP_dV = np.zeros(len(g))
+    dP_dV[:-1] = r.dP_shell[:len(g) - 1] / dV
+    return s, u, P_beam, dP_dV, float(r.P_dep[0])
+
+
+def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
+              steering_angle_pol: float, spot_size: float, inverse_curvature_radius: float,
+              f: float, mode: int, s_max: float, psi_dP_dV, *, ds: float = 1e-4,
+              traj_stride: int = 1, **kwargs):
+    """make_beam (src/solve.jl:209-242) -> (arc_lengths, trajectories, ray_powers, dP_dV,
+    deposited_power, ray_weights).  kwargs go to launch_peripheral_rays."""
+    omega = 2.0 * np.pi * f
+    N0 = pol_tor_angles_2_vector(steering_angle_pol, steering_angle_tor)
+    x0 = np.array([r * np.cos(phi), r * np.sin(phi), z])
+    pos, dirs, w = launch_peripheral_rays(x0, N0, spot_size, inverse_curvature_radius, f, **kwargs)
+    xp, Np, s0, st = ray_entry(plasma, pos, dirs, omega, mode)
+    bad = np.flatnonzero(st != OK)
+    if len(bad):
+        raise RayEntryError(f"{len(bad)} rays failed entry, first: ray {bad[0]} "
+                            f"{STATUS_NAMES[st[bad[0]]]}")
+    n_steps = _steps_for(s_max, ds)
+    g = f64(psi_dP_dV)
+    res = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, weights=w,
+                traj_stride=traj_stride)
+    dV = plasma.shell_volumes(g)
+    dP_dV = np.zeros(len(g))
+    dP_dV[:-1] = res.dP_shell[:len(g) - 1] / dV
+    deposited_power = float(res.dP_shell[len(g)])
+    arc_lengths, trajectories, ray_powers = [], [], []
+    for i in range(len(w)):
+        k = int(res.steps[i]) // traj_stride
+        arc_lengths.append(np.concatenate([[0.0, s0[i]], s0[i] + ds * traj_stride * np.arange(1, k + 1)]))
+        trajectories.append(np.vstack([pos[i][None], xp[i][None], res.traj[i, :k, :3]]))
+        ray_powers.append(np.concatenate([[1.0, 1.0], np.exp(-res.traj[i, :k, 3])]))
+    return arc_lengths, trajectories, ray_powers, dP_dV, deposited_power, w
