@@ -201,8 +201,15 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+#ifndef TORJ_BLOCK
+#define TORJ_BLOCK 256
+#endif
+#ifndef TORJ_MIN_WAVES
+#define TORJ_MIN_WAVES 2
+#endif
+
 template <bool ABS, bool DEPO, bool TRAJ>
-__global__ void __launch_bounds__(256, 2) k_trace(TraceArgs a) {
+__global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i < a.n;
     const GLTable &gl = c_gl;
@@ -1220,7 +1227,7 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
         if (a.n_save > 0)
             HIPCK(hipMemsetAsync(traj, 0xFF, (size_t)a.n_save * 4 * n * sizeof(double), s));  // NaN
     }
-    const dim3 grd(nblocks(n, 256)), blk(256);
+    const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
 #define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
     if (cfg->absorption) {
         if (depo) {

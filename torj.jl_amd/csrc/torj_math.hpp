@@ -307,7 +307,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
 // Albajar absorption, src/absorption.jl:10-64, 132-226
 // ---------------------------------------------------------------------------
 constexpr int kMaxGL = 64;
-constexpr int kSeriesFast = 15;   // Horner terms, exact to < 1e-17 rel. for arg <= 4
+constexpr int kSeriesFast = 16;   // Horner terms, truncation < 2^-58 rel. for arg <= 4
 constexpr int kSeriesSlow = 44;   // arg <= 12
 constexpr double kArgFast = 4.0;
 constexpr double kArgSlow = 12.0;
@@ -325,10 +325,27 @@ struct GLTable {
     double t[kMaxGL], w[kMaxGL], st[kMaxGL];  // nodes, weights, sqrt(1-t^2)
 };
 
-// Horner evaluation of S_nu and S_{nu+1} at z; K terms.  Coefficient table
-// kSeries[nu-2][k] (nu = 2..4) lives in constant memory on the device (uniform
-// scalar loads) instead of being materialised as 64-bit immediates.
-constexpr int kSeriesMax = 44;
+#ifndef TORJ_NODE_UNROLL
+#define TORJ_NODE_UNROLL 1
+#endif
+
+// Horner evaluation of S_nu and S_{nu+1} at z with K terms; coefficients are
+// compile-time immediates (one v_fma_f64 each, constant operand in SGPRs).
+template <int K, int NU>
+TORJ_HD void series_pair(double z, double &Sa, double &Sb) {
+    double a = series_coef(NU, K - 1), b = series_coef(NU + 1, K - 1);
+#pragma unroll
+    for (int k = K - 2; k >= 0; k--) {
+        a = fma(a, z, series_coef(NU, k));
+        b = fma(b, z, series_coef(NU + 1, k));
+    }
+    Sa = a;
+    Sb = b;
+}
+
+// Slow path (arg > 4, unphysical for |N| <= 1): rolled loop over a
+// constant-memory coefficient table so it costs no registers in the hot path.
+constexpr int kSeriesMax = kSeriesSlow;
 struct SeriesTable {
     double c[3][kSeriesMax];
 };
@@ -344,12 +361,12 @@ __constant__ constexpr SeriesTable kSeriesTab = make_series_table();
 constexpr SeriesTable kSeriesTab = make_series_table();
 #endif
 
-template <int K, int NU>
-TORJ_HD void series_pair(double z, double &Sa, double &Sb) {
+template <int NU>
+TORJ_HD void series_pair_loop(double z, double &Sa, double &Sb) {
     const double *ca = kSeriesTab.c[NU - 2], *cb = kSeriesTab.c[NU - 1];
-    double a = ca[K - 1], b = cb[K - 1];
-#pragma unroll 7
-    for (int k = K - 2; k >= 0; k--) {
+    double a = ca[kSeriesSlow - 1], b = cb[kSeriesSlow - 1];
+#pragma unroll 1
+    for (int k = kSeriesSlow - 2; k >= 0; k--) {
         a = fma(a, z, ca[k]);
         b = fma(b, z, cb[k]);
     }
@@ -357,18 +374,60 @@ TORJ_HD void series_pair(double z, double &Sa, double &Sb) {
     Sb = b;
 }
 
-template <int NU>
-TORJ_HD void series_pair_any(double arg, double z, double &Sa, double &Sb) {
-    // arg = x_m sqrt(1-t^2) < m for |N| <= 1 (x_m < m N_perp / sqrt(1-N_par^2)),
-    // so the 15-term branch is the only one taken on physical rays; the
-    // 44-term branch keeps full accuracy up to arg ~ 12 (no function calls:
-    // a call in the node loop would force the whole RK4 state through the
-    // call ABI / scratch).
-    if (arg <= kArgFast) {
-        series_pair<kSeriesFast, NU>(z, Sa, Sb);
-    } else {
-        series_pair<kSeriesSlow, NU>(z, Sa, Sb);
+// Per-harmonic constants of the node sum (abs_Al_pol_fact / abs_Al_integral_nume_fast)
+struct HarmConst {
+    double x_m, K0, K1, K2, K3, K4, K5, upa0, upa1, r2m1, mu;
+};
+
+// A symmetric pair of Gauss-Legendre nodes (+t, -t): w * pol_fact * exp(mu (1 -
+// gamma)) summed over both, without the node-independent factor (-mu) (m / (N_perp
+// omega_bar))^2.  GL nodes are symmetric with equal weights, and the Bessel
+// argument x_m sqrt(1-t^2) is even in t, so the Bessel factors (2 Horner series
+// S_m, S_{m+1} of K terms + the downward recurrence S_{m-1} = m S_m + z S_{m+1})
+// are computed once per pair.  With `single`, only the +t node is taken (the
+// middle node of an odd-order rule, t = 0).
+template <int M, int K>
+TORJ_HD double pair_term(const HarmConst &c, double t, double st, double w, bool single) {
+    constexpr double md = (double)M;
+    const double arg = c.x_m * st;
+    const double h = 0.5 * arg;
+    const double h2 = h * h;
+    double Sm, Sm1;
+    if constexpr (K > 0)
+        series_pair<K, M>(-h2, Sm, Sm1);
+    else
+        series_pair_loop<M>(-h2, Sm, Sm1);
+    const double Sl = md * Sm - h2 * Sm1;
+    double p = h;  // h^(2m-1)
+#pragma unroll
+    for (int k = 1; k < 2 * M - 1; k++) p *= h;
+    const double A = h * (Sm * Sm);
+    const double B = h * (c.K2 * h2 * Sl * Sm1);
+    const double Cc = st * Sm * (Sl - h2 * Sm1);
+    const double wp = w * p;
+    const double u_perp1 = 1.0 + c.r2m1 * (1.0 - t * t);
+    // +t
+    const double brp = A * fma(t, fma(c.K3, t, c.K4), c.K0) - B + Cc * fma(c.K5, t, c.K1);
+    const double upp = fma(c.upa1, t, c.upa0);
+    const double gp = sqrt(fma(upp, upp, u_perp1));
+    double r = (wp * brp) * exp(c.mu * (1.0 - gp));
+    if (!single) {  // -t
+        const double brm = A * fma(-t, fma(-c.K3, t, c.K4), c.K0) - B + Cc * fma(-c.K5, t, c.K1);
+        const double upm = fma(-c.upa1, t, c.upa0);
+        const double gm = sqrt(fma(upm, upm, u_perp1));
+        r += (wp * brm) * exp(c.mu * (1.0 - gm));
     }
+    return r;
+}
+
+template <int M, int K>
+TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
+    const int n = gl.n, half = n >> 1;
+    double acc = 0.0;
+#pragma unroll 1
+    for (int i = 0; i < half; i++) acc += pair_term<M, K>(c, gl.t[i], gl.st[i], gl.w[i], false);
+    if (n & 1) acc += pair_term<M, K>(c, gl.t[half], gl.st[half], gl.w[half], true);
+    return acc;
 }
 
 struct AlbajarWork {
@@ -377,46 +436,42 @@ struct AlbajarWork {
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
-// abs_Al_pol_fact), returned WITHOUT the Maxwellian normalisation a*(mu/2pi)^1.5
+// abs_Al_pol_fact) times sqrt((m/m_0)^2 - 1), WITHOUT the Maxwellian
+// normalisation a*(mu/2pi)^1.5 (common to both harmonics).
 template <int M>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
                                 double inv_sqNp, double sqNp, double N_perp, double omega_bar,
                                 double Axz, double ea, double e3) {
     constexpr double md = (double)M;
-    const double r2m1 = r * r - 1.0;
-    const double sq_r = sqrt(r2m1);
-    const double x_m = N_perp * omega_bar * sq_r;
-    const double q = x_m / (md * sqNp);
-    const double K0 = Axz * Axz + ea * ea;
-    const double K1 = Axz * ea * x_m / md;
-    const double K2 = 4.0 * ea * ea / (md * md);
-    const double K3 = q * q * e3 * e3;
-    const double K4 = 2.0 * q * Axz * e3;
-    const double K5 = q * ea * e3 * x_m / md;
-    const double upa0 = inv_sqNp * r * Npar, upa1 = inv_sqNp * sq_r;
-    double sum = 0.0;
-#pragma unroll 1
-    for (int i = 0; i < gl.n; i++) {
-        const double t = gl.t[i], st = gl.st[i];
-        const double arg = x_m * st;
-        const double h = 0.5 * arg;
-        const double h2 = h * h;
-        double Sm, Sm1;
-        series_pair_any<M>(arg, -h2, Sm, Sm1);
-        const double Sl = md * Sm - h2 * Sm1;  // S_{m-1} = m S_m + z S_{m+1}
-        // h^(2m-1)
-        double p = h;
-#pragma unroll
-        for (int k = 1; k < 2 * M - 1; k++) p *= h;
-        const double Jn2 = Sm * Sm;
-        const double bracket =
-            h * (Jn2 * fma(t, fma(K3, t, K4), K0) - K2 * h2 * Sl * Sm1) +
-            st * Sm * (Sl - h2 * Sm1) * fma(K5, t, K1);
-        const double pol = p * bracket;
-        const double u_par = fma(upa1, t, upa0);
-        const double u_perp_sq = r2m1 * (1.0 - t * t);
-        const double gamma = sqrt(1.0 + u_par * u_par + u_perp_sq);
-        sum = fma(gl.w[i] * pol, exp(mu * (1.0 - gamma)), sum);
+    HarmConst c;
+    c.r2m1 = r * r - 1.0;
+    const double sq_r = sqrt(c.r2m1);
+    c.x_m = N_perp * omega_bar * sq_r;
+    const double q = c.x_m / (md * sqNp);
+    c.K0 = Axz * Axz + ea * ea;
+    c.K1 = Axz * ea * c.x_m / md;
+    c.K2 = 4.0 * ea * ea / (md * md);
+    c.K3 = q * q * e3 * e3;
+    c.K4 = 2.0 * q * Axz * e3;
+    c.K5 = q * ea * e3 * c.x_m / md;
+    c.upa0 = inv_sqNp * r * Npar;
+    c.upa1 = inv_sqNp * sq_r;
+    c.mu = mu;
+    // Series length from the largest Bessel argument x_m (truncation < 2^-58
+    // relative, checked with mpmath in tests): x_m <= 1: 9 terms, <= 2: 12,
+    // <= 3: 14, <= 4: 16; physical rays have x_m < m.  The level is made
+    // wave-uniform (max over the active lanes) so the node loop does not diverge.
+    int level = c.x_m <= 1.0 ? 0 : (c.x_m <= 2.0 ? 1 : (c.x_m <= 3.0 ? 2 : (c.x_m <= kArgFast ? 3 : 4)));
+#ifdef __HIP_DEVICE_COMPILE__
+    level = __ballot(level == 4) ? 4 : (__ballot(level == 3) ? 3 : (__ballot(level == 2) ? 2 : (__ballot(level == 1) ? 1 : 0)));
+#endif
+    double sum;
+    switch (level) {
+        case 0: sum = node_sum<M, 9>(gl, c); break;
+        case 1: sum = node_sum<M, 12>(gl, c); break;
+        case 2: sum = node_sum<M, 14>(gl, c); break;
+        case 3: sum = node_sum<M, 16>(gl, c); break;
+        default: sum = node_sum<M, 0>(gl, c); break;
     }
     const double Pm = md / (N_perp * omega_bar);
     return -mu * Pm * Pm * sum * sq_r;

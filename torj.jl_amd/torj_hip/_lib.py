@@ -14,7 +14,7 @@ import numpy as np
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 _ROOT = os.path.dirname(_PKG)  # torj.jl_amd/
-LIB_PATH = os.path.join(_ROOT, "build", "libtorj_hip.so")
+LIB_PATH = os.environ.get("TORJ_HIP_LIB") or os.path.join(_ROOT, "build", "libtorj_hip.so")
 CSRC = os.path.join(_ROOT, "csrc")
 
 _dp = C.POINTER(C.c_double)
