@@ -61,6 +61,7 @@ def main():
     import torj_hip as T
     from torj_hip import flops as F
     from torj_hip import synthetic as S
+    from torj_hip.parallel import allreduce_deposition
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -103,7 +104,7 @@ def main():
     d_Pdep = torch.empty(n, dtype=torch.float64, device=dev)
     n_save = args.n_steps // args.traj_stride if args.traj_stride > 0 else 0
     d_traj = torch.empty((max(n_save, 1), 4, n), dtype=torch.float64, device=dev)
-    d_cnt = torch.zeros(4, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(5, dtype=torch.int64, device=dev)
     cfg = T._lib.TraceCfg(omega, args.mode, args.ds, args.n_steps, max(1, args.n_steps // 100),
                           1.0, 1e-6, 1, args.traj_stride)
     L = T.lib()
@@ -124,7 +125,7 @@ def main():
         if ev is not None:
             ev[1].record(stream)
         if world > 1:
-            dist.all_reduce(d_dP)  # RCCL over xGMI: (n_psi+1) fp64, make_beam's reduce
+            allreduce_deposition(d_dP)  # RCCL over xGMI: (n_psi+1) fp64, make_beam's reduce
 
     # counted launch (work counters for the algorithmic FLOP figure), also warms up
     d_cnt.zero_()
@@ -204,7 +205,8 @@ def main():
                 "flop_per_ray_step": flop / max(cnt[0], 1),
             },
             "work_counters": {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
-                              "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3])},
+                              "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
+                              "bessel_series_terms": int(cnt[4])},
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
@@ -221,8 +223,7 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid):
 
     OP = O.OraclePlasma(*S.plasma_args(eq))
     O.abs_al_init(24)
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)
-    threads = min(threads, os.cpu_count() or 1)
+    threads = O.default_threads()
     idx = np.linspace(0, len(w) - 1, num=threads, dtype=int)  # calibration sample
     t0 = time.perf_counter()
     r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, psi_grid=grid,

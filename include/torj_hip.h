@@ -159,9 +159,9 @@ int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *
 
 /* Device-pointer form (inputs resident in HBM; what bench.py times).
  * dP_shell (n_psi+1) is ACCUMULATED into (zero it first).  counters (may be
- * NULL): 4 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
- * reaching the harmonic sum, harmonic integrals -- the basis of the algorithmic
- * FLOP count.  stream: hipStream_t or NULL. */
+ * NULL): 5 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
+ * reaching the harmonic sum, harmonic integrals, Bessel-series terms -- the
+ * basis of the algorithmic FLOP count.  stream: hipStream_t or NULL. */
 int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                       const double *N0, const double *weights, int n_psi,
                       const double *psi_grid, double *state, int *status, int *steps,

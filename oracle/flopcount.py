@@ -182,8 +182,14 @@ def _series_coef(nu, k):
     return 1.0 / (math.factorial(k) * math.factorial(k + nu))
 
 
+def series_terms(x_m):
+    """series length rule of torj_math.hpp (albajar_harmonic)"""
+    return 9 if x_m <= 1.0 else 12 if x_m <= 2.0 else 14 if x_m <= 3.0 else 16 if x_m <= 4.0 else 44
+
+
 def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, sqNp, Nperp, omega_bar, Axz, ea, e3, m,
-                     K=15, count=None):
+                     count=None):
+    """Node-pair form of abs_Al_integral_nume_fast x sqrt((m/m0)^2-1) (torj_math.hpp)."""
     md = float(m)
     r2m1 = r * r - 1.0
     sq_r = sqrt(r2m1)
@@ -196,33 +202,44 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, sqNp, Nperp, omega_bar, Axz, ea,
     K4 = 2.0 * q * Axz * e3
     K5 = q * ea * e3 * x_m / md
     upa0, upa1 = inv_sqNp * r * Npar, inv_sqNp * sq_r
+    K = series_terms(x_m.v)
     if count is not None:
         count["harm_setup"] = Counter.n - count["_t0"]
     total = CF(0)
-    for t, w, st in gl:
-        n0 = Counter.n
+    n = len(gl)
+    for i in range(n // 2 + (n & 1)):
+        t, w, st = gl[i]
+        single = (n & 1) and i == n // 2
         arg = x_m * st
         h = 0.5 * arg
         h2 = h * h
         z = -h2
+        n0 = Counter.n
         Sm, Sm1 = CF(_series_coef(m, K - 1)), CF(_series_coef(m + 1, K - 1))
         for k in range(K - 2, -1, -1):
             Sm = Sm * z + _series_coef(m, k)
             Sm1 = Sm1 * z + _series_coef(m + 1, k)
+        n_series = Counter.n - n0
         Sl = md * Sm - h2 * Sm1
         p = h
         for _ in range(1, 2 * m - 1):
             p = p * h
-        Jn2 = Sm * Sm
-        bracket = h * (Jn2 * (t * (K3 * t + K4) + K0) - K2 * h2 * Sl * Sm1) + \
-            st * Sm * (Sl - h2 * Sm1) * (K5 * t + K1)
-        pol = p * bracket
-        u_par = upa1 * t + upa0
-        u_perp_sq = r2m1 * (1.0 - t * t)
-        gamma = sqrt(1.0 + u_par * u_par + u_perp_sq)
-        total = total + (w * pol) * exp(mu * (1.0 - gamma))
-        if count is not None:
-            count.setdefault("node", []).append(Counter.n - n0)
+        A = h * (Sm * Sm)
+        B = h * (K2 * h2 * Sl * Sm1)
+        Cc = st * Sm * (Sl - h2 * Sm1)
+        wp = w * p
+        u_perp1 = 1.0 + r2m1 * (1.0 - t * t)
+        n1 = Counter.n
+        for tt in ((t,) if single else (t, -t)):
+            br = A * (tt * (K3 * tt + K4) + K0) - B + Cc * (K5 * tt + K1)
+            up = upa1 * tt + upa0
+            g = sqrt(up * up + u_perp1)
+            total = total + (wp * br) * exp(mu * (1.0 - g))
+            if count is not None and "node" not in count:
+                count["node"] = Counter.n - n1
+        if count is not None and "pair_shared" not in count:
+            count["pair_shared"] = (Counter.n - n0) - n_series - (2 - bool(single)) * count["node"]
+            count["term"] = n_series / (K - 1)
     n1 = Counter.n
     Pm = md / (Nperp * omega_bar)
     res = -mu * Pm * Pm * total * sq_r
@@ -277,12 +294,14 @@ def abs_albajar_fast(gl, omega, X, Y, Nabs, Npar, Te, mode, count=None):
     if count is not None:
         count["alpha_pre"] = Counter.n - count["_t0"]
     c_abs = CF(0)
+    hc = count  # per-harmonic figures from the first harmonic only
     for m in (2, 3):
         if not (m < m0):
-            if count is not None:
-                count["_t0"] = Counter.n
+            if hc is not None:
+                hc["_t0"] = Counter.n
             c_abs = c_abs + albajar_harmonic(gl, mu, m / m0, Npar, inv_sqNp, sqNp, Nperp,
-                                             omega_bar, Axz, ea, e3, m, count=count)
+                                             omega_bar, Axz, ea, e3, m, count=hc)
+            hc = None
     n1 = Counter.n
     a = 1.0 / (1.0 + 105.0 / (128.0 * mu * mu) + 15.0 / (8.0 * mu))
     sm = sqrt(mu / (2.0 * math.pi))
@@ -365,9 +384,10 @@ if __name__ == "__main__":
         "FLOPS_RHS_COLD": m["cold"],
         "FLOPS_ALPHA_PRE": m["alpha_pre"],
         "FLOPS_ALPHA_POST": m["alpha_post"],
-        "FLOPS_HARM_SETUP": m["harm_setup"],
-        "FLOPS_HARM_POST": m["harm_post"],
-        "FLOPS_NODE": {2: m["node"][0], 3: m["node"][-1]},
+        "FLOPS_HARM": m["harm_setup"] + m["harm_post"],
+        "FLOPS_PAIR_SHARED": m["pair_shared"],
+        "FLOPS_NODE": m["node"],
+        "FLOPS_SERIES_TERM": m["term"],
         "FLOPS_STEP_OVERHEAD": n_rk + psi_eval,
         "check": {"alpha_counted": m["alpha"], "alpha_oracle": OP.alpha_approx(x, N, om, 1),
                   "du_counted": m["du"], "du_oracle": list(OP.grad_lambda(x, N, om, 1))},

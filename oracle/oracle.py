@@ -18,6 +18,12 @@ _LIB_PATH = os.path.join(_HERE, "build", "libtorj_oracle.so")
 OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL = range(6)
 
 
+def default_threads() -> int:
+    """OMP_NUM_THREADS if set (16 on the GPU box), else up to 8 host cores."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env if env > 0 else min(os.cpu_count() or 1, 8)
+
+
 def build(force: bool = False) -> str:
     if force or not os.path.exists(_LIB_PATH):
         subprocess.check_call(["make", "-s", "-C", _HERE])
@@ -189,7 +195,7 @@ class OraclePlasma:
         n_save = n_steps // traj_stride if traj_stride > 0 else 0
         traj = np.full((n, max(n_save, 1), 4), np.nan)
         w = _c(weights) if weights is not None else None
-        nt = n_threads or os.cpu_count() or 1
+        nt = n_threads or default_threads()
         lib().or_trace(self.ref, C.byref(cfg), n, _p(x0), _p(N0), _p(w) if w is not None else None,
                        _p(state), status.ctypes.data_as(_ip), steps.ctypes.data_as(_ip), _p(dP),
                        _p(Pdep), _p(traj), nt)

@@ -213,7 +213,7 @@ __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs 
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const bool live = i < a.n;
     const GLTable &gl = c_gl;
-    AlbajarWork work = {0u, 0u};
+    AlbajarWork work = {0u, 0u, 0u};
     int steps = 0;
     if (live) {
         double x[3], N[3];
@@ -327,11 +327,13 @@ __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs 
         const unsigned long long s0 = wave_sum((unsigned long long)steps);
         const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
         const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
+        const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
         if ((threadIdx.x & 63) == 0) {
             atomicAdd(a.counters + 0, s0);
             atomicAdd(a.counters + 1, 4ull * s0);
             atomicAdd(a.counters + 2, s2);
             atomicAdd(a.counters + 3, s3);
+            atomicAdd(a.counters + 4, s4);
         }
     }
 }

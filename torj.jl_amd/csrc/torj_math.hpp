@@ -433,6 +433,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
 struct AlbajarWork {
     uint32_t n_active;  // calls that reached the harmonic loop
     uint32_t n_harm;    // harmonic integrals evaluated
+    uint32_t n_terms;   // Bessel-series terms evaluated (sum over node pairs of K)
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
@@ -441,7 +442,7 @@ struct AlbajarWork {
 template <int M>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
                                 double inv_sqNp, double sqNp, double N_perp, double omega_bar,
-                                double Axz, double ea, double e3) {
+                                double Axz, double ea, double e3, AlbajarWork *work) {
     constexpr double md = (double)M;
     HarmConst c;
     c.r2m1 = r * r - 1.0;
@@ -465,6 +466,10 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 #ifdef __HIP_DEVICE_COMPILE__
     level = __ballot(level == 4) ? 4 : (__ballot(level == 3) ? 3 : (__ballot(level == 2) ? 2 : (__ballot(level == 1) ? 1 : 0)));
 #endif
+    if (work) {
+        constexpr int kTerms[5] = {9, 12, 14, kSeriesFast, kSeriesSlow};
+        work->n_terms += (uint32_t)(kTerms[level] * ((gl.n + 1) >> 1));
+    }
     double sum;
     switch (level) {
         case 0: sum = node_sum<M, 9>(gl, c); break;
@@ -526,12 +531,12 @@ TORJ_HD double abs_albajar_fast(const GLTable &gl, double omega, double X, doubl
     double c_abs = 0.0;
     if (!(2.0 < m_0)) {
         c_abs += albajar_harmonic<2>(gl, mu, 2.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
-                                     Axz, ea, e3);
+                                     Axz, ea, e3, work);
         if (work) work->n_harm++;
     }
     if (!(3.0 < m_0)) {  // src/absorption.jl:214 `if m < m_0 continue` (NaN m_0 -> NaN, as reference)
         c_abs += albajar_harmonic<3>(gl, mu, 3.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
-                                     Axz, ea, e3);
+                                     Axz, ea, e3, work);
         if (work) work->n_harm++;
     }
     const double a = 1.0 / (1.0 + 105.0 / (128.0 * mu * mu) + 15.0 / (8.0 * mu));
