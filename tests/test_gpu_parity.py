@@ -28,14 +28,26 @@ def test_fields_match_oracle(gpu, T, hplasma, oplasma):
     x, N = _rand_points(3000, 1)
     om = 2 * np.pi * 85.5e9
     out = hplasma.eval_points(x, N, om)
+    # n_e, T_e are exp(spline of the log profile): their relative error is the
+    # absolute error of the log spline sum, bounded by ~1e-15 x its coefficient
+    # scale (|ln n_e| reaches ~900 far outside the plasma)
+    c_ne = np.abs(hplasma.coefs("lnne")).max()
+    c_te = np.abs(hplasma.coefs("lnTe")).max()
+    R = np.hypot(x[:, 0], x[:, 1])
+    inside = ((R >= hplasma.R_coords[0]) & (R <= hplasma.R_coords[-1]) &
+              (x[:, 2] >= hplasma.Z_coords[0]) & (x[:, 2] <= hplasma.Z_coords[-1]))
     for i in range(0, len(x), 7):
+        # Line() extrapolation multiplies rounding by (distance outside) / (grid step)
+        k = 1e-13 if inside[i] else 1e-11  # host prefilters (Thomas vs LU) differ ~4e-14 rel in ln Te
         B = oplasma.B_spline(x[i])
         assert np.abs(out[0:3, i] - B).max() <= 1e-13 * np.linalg.norm(B)
-        assert rel_err(out[3, i], oplasma.n_e(x[i]), 1e-300) < 1e-12
-        assert rel_err(out[4, i], oplasma.T_e(x[i]), 1e-300) < 1e-12
+        ne, Te = oplasma.n_e(x[i]), oplasma.T_e(x[i])
+        assert rel_err(out[3, i], ne, 1e-300) < k * c_ne
+        assert rel_err(out[4, i], Te, 1e-300) < k * c_te
         assert abs(out[5, i] - oplasma.evaluate("psi", x[i])) < 1e-13 * max(1, abs(out[5, i]))
         X, Y, Npar, b = oplasma.eval_plasma(x[i], N[i], om)
-        assert rel_err(out[6, i], X, 1e-300) < 1e-12 and rel_err(out[7, i], Y) < 1e-13
+        assert rel_err(out[6, i], X, 1e-300) < k * c_ne
+        assert rel_err(out[7, i], Y) < 1e-13
         assert abs(out[8, i] - Npar) < 1e-13 and np.abs(out[9:12, i] - b).max() < 1e-14
     # the single-point API mirrors the reference call shapes
     B1 = T.B_spline(hplasma, x[0])
@@ -187,10 +199,12 @@ def test_trace_termination_statuses(gpu, T, hplasma, oplasma, eq):
     pos, dirs, w = T.launch_peripheral_rays([2.5, 0, 0.4], Nv, s["spot_size"],
                                             s["inverse_curvature_radius"], 92.5e9, N_rings=4)
     xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1)
-    g = T.trace(hplasma, xp, Np, om, 1, n_steps=10000)
-    o = oplasma.trace(xp, Np, om, 1, 1e-4, 10000)
+    # (P_min raised from the reference's 1e-6 so that every ray trips it)
+    g = T.trace(hplasma, xp, Np, om, 1, n_steps=10000, P_min=1e-2)
+    o = oplasma.trace(xp, Np, om, 1, 1e-4, 10000, P_min=1e-2)
     _compare_trace(g, o)
     assert T.ABSORBED in g.status.tolist()
+    assert np.all(g.steps[g.status == T.ABSORBED] % 100 == 0)  # chunk-boundary checks
 
 
 def test_trace_nonuniform_psi_grid(gpu, T, hplasma, oplasma, fan_states):
