@@ -143,59 +143,90 @@ void or_gauss_legendre(int n, double *x, double *w) {
     }
 }
 
-static int cmp_dbl2(const void *a, const void *b) {
-    double x = ((const double *)a)[0], y = ((const double *)b)[0];
-    return (x > y) - (x < y);
+/* Orthonormal Hermite recurrence p_0 = pi^(-1/4), p_{j+1} = z sqrt(2/(j+1)) p_j -
+ * sqrt(j/(j+1)) p_{j-1}, rescaled by 2^-500 whenever it grows past 2^500 (the
+ * exponent is returned in *e2): overflow-free for any n. */
+static void herm_rec(int n, double z, double *pn, double *pn1, int *e2) {
+    double p1 = 0.7511255444649425, p2 = 0.0;
+    int e = 0;
+    for (int j = 0; j < n; j++) {
+        double p3 = p2;
+        p2 = p1;
+        p1 = z * sqrt(2.0 / (j + 1)) * p2 - sqrt((double)j / (j + 1)) * p3;
+        if (fabs(p1) > 0x1p500) {
+            p1 = ldexp(p1, -500);
+            p2 = ldexp(p2, -500);
+            e += 500;
+        }
+    }
+    *pn = p1;
+    *pn1 = p2;
+    *e2 = e;
 }
 
 /* FastGaussQuadrature.gausshermite(n): ascending nodes, weight exp(-x^2)
- * (called from src/launch.jl:72).  Newton on orthonormal Hermite recurrence. */
+ * (called from src/launch.jl:72).  Positive zeros bracketed by sign changes on
+ * a grid finer than the smallest zero spacing (~pi/sqrt(2n+1), near the
+ * origin), bisected, then Newton-polished; w = 2 / (2n p_{n-1}^2). */
 void or_gauss_hermite(int n, double *x, double *w) {
-    const double PIM4 = 0.7511255444649425; /* pi^(-1/4) */
-    int m = (n + 1) / 2;
-    double *xd = (double *)malloc(sizeof(double) * n);
-    double *wd = (double *)malloc(sizeof(double) * n);
-    double z = 0, z1, pp = 0;
-    for (int i = 0; i < m; i++) {
-        if (i == 0)
-            z = sqrt(2.0 * n + 1.0) - 1.85575 * pow(2.0 * n + 1.0, -0.16667);
-        else if (i == 1)
-            z -= 1.14 * pow((double)n, 0.426) / z;
-        else if (i == 2)
-            z = 1.86 * z - 0.86 * xd[0];
-        else if (i == 3)
-            z = 1.91 * z - 0.91 * xd[1];
-        else
-            z = 2.0 * z - xd[i - 2];
-        for (int it = 0; it < 200; it++) {
-            double p1 = PIM4, p2 = 0.0;
-            for (int j = 0; j < n; j++) {
-                double p3 = p2;
-                p2 = p1;
-                p1 = z * sqrt(2.0 / (j + 1)) * p2 - sqrt((double)j / (j + 1)) * p3;
+    int half = n / 2, k = 0;
+    double *pos = (double *)malloc(sizeof(double) * (half + 1));
+    double *pw = (double *)malloc(sizeof(double) * (half + 1));
+    const double zmax = sqrt(2.0 * n + 1.0) + 1.0;
+    const double dz = 0.2 * PI / sqrt(2.0 * n + 1.0);
+    double a = (n & 1) ? 0.5 * dz : 0.0, fa, fa1;
+    int ea;
+    herm_rec(n, a, &fa, &fa1, &ea);
+    while (k < half && a < zmax) {
+        double b = a + dz, fb, fb1;
+        int eb;
+        herm_rec(n, b, &fb, &fb1, &eb);
+        if ((fa > 0) != (fb > 0) && fb != 0.0) {
+            double lo = a, hi = b, flo = fa;
+            for (int it = 0; it < 60; it++) {
+                double m = 0.5 * (lo + hi), fm, fm1;
+                int em;
+                herm_rec(n, m, &fm, &fm1, &em);
+                if ((fm > 0) == (flo > 0)) {
+                    lo = m;
+                    flo = fm;
+                } else {
+                    hi = m;
+                }
             }
-            pp = sqrt(2.0 * n) * p2;
-            z1 = z;
-            z = z1 - p1 / pp;
-            if (fabs(z - z1) <= 1e-15 * fmax(1.0, fabs(z))) break;
+            double z = 0.5 * (lo + hi), pn, pn1;
+            int e;
+            for (int it = 0; it < 3; it++) {
+                herm_rec(n, z, &pn, &pn1, &e);
+                z -= pn / (sqrt(2.0 * n) * pn1);
+            }
+            herm_rec(n, z, &pn, &pn1, &e);
+            pos[k] = z;
+            pw[k] = ldexp(1.0 / (n * pn1 * pn1), -2 * e);
+            k++;
         }
-        xd[i] = z;
-        xd[n - 1 - i] = -z;
-        wd[i] = wd[n - 1 - i] = 2.0 / (pp * pp);
+        a = b;
+        fa = fb;
     }
-    double *pr = (double *)malloc(sizeof(double) * 2 * n);
-    for (int i = 0; i < n; i++) {
-        pr[2 * i] = xd[i];
-        pr[2 * i + 1] = wd[i];
+    int m = 0;
+    for (int i = k - 1; i >= 0; i--, m++) {
+        x[m] = -pos[i];
+        w[m] = pw[i];
     }
-    qsort(pr, n, 2 * sizeof(double), cmp_dbl2);
-    for (int i = 0; i < n; i++) {
-        x[i] = pr[2 * i];
-        w[i] = pr[2 * i + 1];
+    if (n & 1) {
+        double pn, pn1;
+        int e;
+        herm_rec(n, 0.0, &pn, &pn1, &e);
+        x[m] = 0.0;
+        w[m] = ldexp(1.0 / (n * pn1 * pn1), -2 * e);
+        m++;
     }
-    free(pr);
-    free(xd);
-    free(wd);
+    for (int i = 0; i < k; i++, m++) {
+        x[m] = pos[i];
+        w[m] = pw[i];
+    }
+    free(pos);
+    free(pw);
 }
 
 /* ------------------------------------------------------------------------- */

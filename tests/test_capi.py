@@ -57,7 +57,8 @@ def test_plasma_from_coefs_roundtrip(T, hplasma, eq):
 
 def test_launch_fan_matches_oracle(T, O):
     for kw in ({}, {"N_rings": 14, "min_azimuthal_points": 5},
-               {"N_rings": 21, "min_azimuthal_points": 11, "normalize_weight_sum": False}):
+               {"N_rings": 21, "min_azimuthal_points": 11, "normalize_weight_sum": False},
+               {"N_rings": 150, "min_azimuthal_points": 11}):
         for inv in (1 / 3.99, -1 / 2.0, float("inf")):
             N0 = T.pol_tor_angles_2_vector(np.deg2rad(30), np.deg2rad(5))
             a = T.launch_peripheral_rays([2.5, 0.1, 0.4], N0, 0.0174, inv, 92.5e9, **kw)

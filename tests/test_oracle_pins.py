@@ -23,8 +23,9 @@ def test_gauss_legendre_matches_numpy(O, n):
     assert np.all(np.diff(x) > 0)  # ascending, like FastGaussQuadrature
 
 
-@pytest.mark.parametrize("n", [6, 8, 44, 100, 186])
+@pytest.mark.parametrize("n", [1, 2, 5, 6, 8, 44, 100, 186, 200, 202, 301, 302])
 def test_gauss_hermite_matches_numpy(O, n):
+    """incl. n >= 200 (N_rings >= 99), where asymptotic initial guesses fail"""
     x, w = O.gauss_hermite(n)
     xr, wr = np.polynomial.hermite.hermgauss(n)
     assert np.abs(x - xr).max() < 1e-13

@@ -742,42 +742,86 @@ static int host_refraction(const torj_plasma_s *p, const double pp[3], const dou
 // ===========================================================================
 // launch fan (host), src/launch.jl:24-132
 // ===========================================================================
-// FastGaussQuadrature.gausshermite(n): Newton on the orthonormal Hermite
-// recurrence, asymptotic initial guesses, ascending order.
-static void gauss_hermite(int n, std::vector<double> &x, std::vector<double> &w) {
-    x.assign(n, 0.0);
-    w.assign(n, 0.0);
-    const int m = (n + 1) / 2;
-    std::vector<double> xd(n);
-    double z = 0;
-    for (int i = 0; i < m; i++) {
-        if (i == 0)
-            z = std::sqrt(2.0 * n + 1.0) - 1.85575 * std::pow(2.0 * n + 1.0, -1.0 / 6.0);
-        else if (i == 1)
-            z -= 1.14 * std::pow((double)n, 0.426) / z;
-        else if (i == 2)
-            z = 1.86 * z - 0.86 * xd[0];
-        else if (i == 3)
-            z = 1.91 * z - 0.91 * xd[1];
-        else
-            z = 2.0 * z - xd[i - 2];
-        double pp = 1.0;
-        for (int it = 0; it < 200; it++) {
-            double p1 = 0.7511255444649425, p2 = 0.0;  // pi^(-1/4)
-            for (int j = 0; j < n; j++) {
-                const double p3 = p2;
-                p2 = p1;
-                p1 = z * std::sqrt(2.0 / (j + 1)) * p2 - std::sqrt((double)j / (j + 1)) * p3;
-            }
-            pp = std::sqrt(2.0 * n) * p2;
-            const double dz = p1 / pp;
-            z -= dz;
-            if (std::fabs(dz) <= 1e-15 * std::max(1.0, std::fabs(z))) break;
+// Orthonormal Hermite recurrence, rescaled by 2^-500 past 2^500 (overflow-free
+// for any n); returns p_n, p_{n-1} and the binary exponent of the scale.
+static void herm_rec(int n, double z, double &pn, double &pn1, int &e2) {
+    double p1 = 0.7511255444649425, p2 = 0.0;  // pi^(-1/4)
+    int e = 0;
+    for (int j = 0; j < n; j++) {
+        const double p3 = p2;
+        p2 = p1;
+        p1 = z * std::sqrt(2.0 / (j + 1)) * p2 - std::sqrt((double)j / (j + 1)) * p3;
+        if (std::fabs(p1) > 0x1p500) {
+            p1 = std::ldexp(p1, -500);
+            p2 = std::ldexp(p2, -500);
+            e += 500;
         }
-        xd[i] = z;
-        x[n - 1 - i] = z;
-        x[i] = -z;
-        w[i] = w[n - 1 - i] = 2.0 / (pp * pp);
+    }
+    pn = p1;
+    pn1 = p2;
+    e2 = e;
+}
+
+// FastGaussQuadrature.gausshermite(n) (src/launch.jl:72): ascending nodes,
+// weight exp(-x^2).  Zeros are bracketed by sign changes on a grid finer than
+// the smallest zero spacing (~pi/sqrt(2n+1), at the origin), bisected and
+// Newton-polished -- robust for every n (asymptotic initial guesses are not).
+static void gauss_hermite(int n, std::vector<double> &x, std::vector<double> &w) {
+    std::vector<double> pos, pw;
+    const int half = n / 2;
+    const double zmax = std::sqrt(2.0 * n + 1.0) + 1.0;
+    const double dz = 0.2 * kPi / std::sqrt(2.0 * n + 1.0);
+    double a = (n & 1) ? 0.5 * dz : 0.0, fa, fa1;
+    int ea;
+    herm_rec(n, a, fa, fa1, ea);
+    while ((int)pos.size() < half && a < zmax) {
+        const double b = a + dz;
+        double fb, fb1;
+        int eb;
+        herm_rec(n, b, fb, fb1, eb);
+        if ((fa > 0) != (fb > 0) && fb != 0.0) {
+            double lo = a, hi = b, flo = fa;
+            for (int it = 0; it < 60; it++) {
+                const double m = 0.5 * (lo + hi);
+                double fm, fm1;
+                int em;
+                herm_rec(n, m, fm, fm1, em);
+                if ((fm > 0) == (flo > 0)) {
+                    lo = m;
+                    flo = fm;
+                } else {
+                    hi = m;
+                }
+            }
+            double z = 0.5 * (lo + hi), pn, pn1;
+            int e;
+            for (int it = 0; it < 3; it++) {
+                herm_rec(n, z, pn, pn1, e);
+                z -= pn / (std::sqrt(2.0 * n) * pn1);
+            }
+            herm_rec(n, z, pn, pn1, e);
+            pos.push_back(z);
+            pw.push_back(std::ldexp(1.0 / (n * pn1 * pn1), -2 * e));
+        }
+        a = b;
+        fa = fb;
+    }
+    x.clear();
+    w.clear();
+    for (int i = (int)pos.size() - 1; i >= 0; i--) {
+        x.push_back(-pos[i]);
+        w.push_back(pw[i]);
+    }
+    if (n & 1) {
+        double pn, pn1;
+        int e;
+        herm_rec(n, 0.0, pn, pn1, e);
+        x.push_back(0.0);
+        w.push_back(std::ldexp(1.0 / (n * pn1 * pn1), -2 * e));
+    }
+    for (size_t i = 0; i < pos.size(); i++) {
+        x.push_back(pos[i]);
+        w.push_back(pw[i]);
     }
 }
 

@@ -1,0 +1,147 @@
+# TorJHIP.jl -- drop-in GPU back end for TorJ.jl's ray-tracing path (make_ray /
+# make_beam, src/solve.jl) on AMD MI355X, through the C ABI of libtorj_hip.so
+# (include/torj_hip.h).  Kept deliberately thin: argument marshalling only.
+#
+# Usage (see INTEGRATION.md):
+#     using TorJ, TorJHIP
+#     TorJHIP.abs_Al_init(24)
+#     gp = TorJHIP.GPUPlasma(R, Z, psi_norm, psi_prof, ne, Te, Br, Bz, Bphi, eq_psi, eq_vol)
+#     s, u, P, dP_dV, P_dep = TorJHIP.make_ray(gp, x0, N0, f, 1, 0.4, psi_dP_dV)
+#
+# Untested in this repository's container (no Julia toolchain); the same ABI is
+# exercised by the Python ctypes mirror in torj.jl_amd/torj_hip.
+module TorJHIP
+
+const libtorj = get(ENV, "TORJ_HIP_LIB", joinpath(@__DIR__, "..", "build", "libtorj_hip.so"))
+
+struct TraceCfg              # torj_trace_cfg
+    omega::Float64
+    mode::Cint
+    ds::Float64
+    n_steps::Cint
+    chunk_steps::Cint
+    psi_exit::Float64
+    P_min::Float64
+    absorption::Cint
+    traj_stride::Cint
+end
+
+check(rc) = rc == 0 || error(unsafe_string(ccall((:torj_last_error, libtorj), Cstring, ())))
+
+"""abs_Al_init(N) -- src/absorption.jl:1-7"""
+abs_Al_init(n::Integer) = check(ccall((:torj_abs_al_init, libtorj), Cint, (Cint,), n))
+
+mutable struct GPUPlasma
+    h::Ptr{Cvoid}
+    psi_prof_max::Float64
+    function GPUPlasma(R::Vector{Float64}, Z::Vector{Float64}, psi_norm::Matrix{Float64},
+                       psi_prof::Vector{Float64}, ne::Vector{Float64}, Te::Vector{Float64},
+                       Br::Matrix{Float64}, Bz::Matrix{Float64}, Bphi::Matrix{Float64},
+                       eq_psi::Vector{Float64}, eq_vol::Vector{Float64}; device::Integer=0)
+        h = Ref{Ptr{Cvoid}}(C_NULL)
+        # Julia matrices are (nR, nZ) column-major: exactly the ABI layout
+        check(ccall((:torj_plasma_create, libtorj), Cint,
+                    (Cint, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Float64},
+                     Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint,
+                     Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Ptr{Cvoid}}),
+                    length(R), length(Z), R, Z, psi_norm, length(psi_prof), psi_prof, ne, Te,
+                    Br, Bz, Bphi, length(eq_psi), eq_psi, eq_vol, device, h))
+        p = new(h[], maximum(psi_prof))
+        finalizer(x -> ccall((:torj_plasma_destroy, libtorj), Cint, (Ptr{Cvoid},), x.h), p)
+        return p
+    end
+end
+
+"""first_point + vacuum_plasma_refraction for n rays (x0, N0: n x 3)."""
+function ray_entry(p::GPUPlasma, x0::Matrix{Float64}, N0::Matrix{Float64}, omega, mode)
+    n = size(x0, 1)
+    xp, Np, s0, st = zeros(n, 3), zeros(n, 3), zeros(n), zeros(Cint, n)
+    check(ccall((:torj_ray_entry, libtorj), Cint,
+                (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Float64, Cint, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Cint}),
+                p.h, n, x0, N0, omega, mode, xp, Np, s0, st))
+    return xp, Np, s0, st
+end
+
+function trace(p::GPUPlasma, cfg::TraceCfg, x0::Matrix{Float64}, N0::Matrix{Float64},
+               w::Vector{Float64}, psi_grid::Vector{Float64})
+    n = size(x0, 1)
+    n_save = cfg.traj_stride > 0 ? cfg.n_steps ÷ cfg.traj_stride : 0
+    state, status, steps = zeros(n, 7), zeros(Cint, n), zeros(Cint, n)
+    dP, Pdep, traj = zeros(length(psi_grid) + 1), zeros(n), zeros(n, 4, max(n_save, 1))
+    GC.@preserve x0 N0 w psi_grid begin
+        check(ccall((:torj_trace, libtorj), Cint,
+                    (Ptr{Cvoid}, Ref{TraceCfg}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                     Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Cint}, Ptr{Cint}, Ptr{Float64},
+                     Ptr{Float64}, Ptr{Float64}),
+                    p.h, cfg, n, x0, N0, w, length(psi_grid), psi_grid, state, status, steps, dP,
+                    Pdep, n_save > 0 ? traj : C_NULL))
+    end
+    return state, status, steps, dP, Pdep, traj
+end
+
+function shell_volumes(p::GPUPlasma, g::Vector{Float64})
+    dV = zeros(length(g) - 1)
+    check(ccall((:torj_shell_volumes, libtorj), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}),
+                p.h, length(g), g, dV))
+    return dV
+end
+
+"""make_ray -- same signature and return tuple as TorJ.make_ray (src/solve.jl:135-181)."""
+function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f::Real,
+                  mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4)
+    ω = 2π * f
+    xp, Np, s0, st = ray_entry(p, reshape(collect(Float64, x0), 1, 3),
+                               reshape(collect(Float64, N_vacuum), 1, 3), ω, mode)
+    st[1] == 0 || throw(AssertionError("ray entry failed (status $(st[1]))"))
+    n_steps = max(1, round(Int, s_max / ds))
+    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1)
+    g = collect(Float64, psi_dP_dV)
+    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, ones(1), g)
+    k = steps[1]
+    s = vcat(0.0, s0[1], s0[1] .+ ds .* (1:k))
+    u = vcat([collect(Float64, x0)], [xp[1, :]], [traj[1, 1:3, i] for i in 1:k])
+    P_beam = vcat(1.0, 1.0, exp.(-traj[1, 4, 1:k]))
+    dP_dV = zeros(length(g))
+    dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, g)
+    return s, u, P_beam, dP_dV, Pdep[1]
+end
+
+"""make_beam -- same signature and return tuple as TorJ.make_beam (src/solve.jl:209-242);
+uses TorJ.launch_peripheral_rays / IMAS angles on the host, the GPU for every ray."""
+function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::Integer,
+                   s_max::Float64, psi_dP_dV::Vector{Float64}; ds::Float64=1e-4,
+                   N_rings::Integer=3, min_azimuthal_points::Integer=5,
+                   normalize_weight_sum::Bool=true)
+    N0 = zeros(3)
+    ccall((:torj_pol_tor_angles_2_vector, libtorj), Cvoid, (Float64, Float64, Ptr{Float64}),
+          pol, tor, N0)
+    x0 = [r * cos(phi), r * sin(phi), z]
+    nr = Ref{Cint}(0)
+    check(ccall((:torj_launch_peripheral_rays, libtorj), Cint,
+                (Ptr{Float64}, Ptr{Float64}, Float64, Float64, Float64, Cint, Cint, Cint, Ref{Cint},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                x0, N0, spot, inv_curv, f, N_rings, min_azimuthal_points, normalize_weight_sum, nr,
+                C_NULL, C_NULL, C_NULL))
+    n = nr[]
+    pos, dirs, w = zeros(n, 3), zeros(n, 3), zeros(n)
+    check(ccall((:torj_launch_peripheral_rays, libtorj), Cint,
+                (Ptr{Float64}, Ptr{Float64}, Float64, Float64, Float64, Cint, Cint, Cint, Ref{Cint},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                x0, N0, spot, inv_curv, f, N_rings, min_azimuthal_points, normalize_weight_sum, nr,
+                pos, dirs, w))
+    ω = 2π * f
+    xp, Np, s0, st = ray_entry(p, pos, dirs, ω, mode)
+    all(st .== 0) || throw(AssertionError("ray entry failed for $(count(st .!= 0)) rays"))
+    n_steps = max(1, round(Int, s_max / ds))
+    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1)
+    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV)
+    dP_dV = zeros(length(psi_dP_dV))
+    dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, psi_dP_dV)
+    arc_lengths = [vcat(0.0, s0[i], s0[i] .+ ds .* (1:steps[i])) for i in 1:n]
+    trajectories = [vcat([pos[i, :]], [xp[i, :]], [traj[i, 1:3, k] for k in 1:steps[i]]) for i in 1:n]
+    ray_powers = [vcat(1.0, 1.0, exp.(-traj[i, 4, 1:steps[i]])) for i in 1:n]
+    return arc_lengths, trajectories, ray_powers, dP_dV, dP[end], w
+end
+
+end # module
