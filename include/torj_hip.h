@@ -168,6 +168,15 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
                       double *dP_shell, double *P_dep, double *traj, uint64_t *counters,
                       void *stream);
 
+/* Scheduling of torj_trace / torj_trace_device launches on this plasma handle
+ * (no reference counterpart: an MI355X tuning knob; results are independent
+ * of it up to the summation order of dP_shell).  mode -1: default (env
+ * TORJ_SCHED; else 1 when the beam has more
+ * 64-ray groups than the device has SIMDs, otherwise 0); 0: one lane per ray for the whole trace; 1: persistent
+ * waves pulling 64-ray groups chunk by chunk from a ready queue.  waves: number
+ * of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
+int torj_set_sched(torj_plasma_t p, int mode, int waves);
+
 /* shell volumes dV[j] = V(psi_grid[j+1]) - V(psi_grid[j]), j < n_psi-1 (host;
  * src/plasma.jl:117-122) */
 int torj_shell_volumes(torj_plasma_t p, int n_psi, const double *psi_grid, double *dV);

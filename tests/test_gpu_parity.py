@@ -162,6 +162,29 @@ def test_trace_matches_oracle_2000_steps(gpu, T, hplasma, oplasma, fan_states, m
         assert np.median(g.P_end) < 0.05  # X2 absorption happens on this path
 
 
+@pytest.mark.parametrize("waves", [1, 3, 0])
+def test_trace_independent_of_scheduling(gpu, T, hplasma, fan_states, waves):
+    """The ready-queue kernel (groups migrate between waves chunk by chunk; 1 and
+    3 waves for 5 groups force every hand-over path) reproduces the one-lane-
+    per-ray kernel bit for bit on every per-ray output; dP_shell differs only by
+    the order of its atomic sums."""
+    xp, Np, w, om = fan_states[1]
+    idx = np.arange(0, len(w), 4)[:260]
+    grid = np.linspace(0, 1, 1000)
+    kw = dict(ds=1e-4, n_steps=2000, psi_grid=grid, weights=w[idx], traj_stride=100)
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp[idx], Np[idx], om, 1, **kw)
+        hplasma.set_sched(1, waves)
+        b = T.trace(hplasma, xp[idx], Np[idx], om, 1, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    for f in ("state", "status", "steps", "P_dep"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-14 * np.abs(a.dP_shell).max()
+
+
 def test_trace_cold_plasma_no_absorption(gpu, T, hplasma, oplasma, fan_states):
     xp, Np, w, om = fan_states[-1]
     g = T.trace(hplasma, xp[:64], Np[:64], om, -1, n_steps=1000, absorption=False)

@@ -121,8 +121,6 @@ struct TraceArgs {
     int *steps;
     int n_psi;
     const double *grid;
-    int grid_uniform;
-    double g0, ginv;
     double *dP;  // n_psi + 1
     double *Pdep;
     int traj_stride;
@@ -134,25 +132,22 @@ struct TraceArgs {
 // psi shell j with grid[j] <= v < grid[j+1], clamped to [0, n-2]; identical
 // result to a binary search on the grid array.
 __device__ __forceinline__ int shell_of(const TraceArgs &a, double v) {
+    // first guess as if the grid were uniform; accept it only if it brackets v,
+    // else binary search: the result equals a binary search for any monotone grid
     const int nm2 = a.n_psi - 2;
-    int j;
-    if (a.grid_uniform) {
-        j = (int)floor((v - a.g0) * a.ginv);
-        j = j < 0 ? 0 : (j > nm2 ? nm2 : j);
-        while (j > 0 && a.grid[j] > v) j--;
-        while (j < nm2 && a.grid[j + 1] <= v) j++;
-    } else {
-        int lo = 0, hi = a.n_psi - 1;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (a.grid[mid] <= v)
-                lo = mid;
-            else
-                hi = mid;
-        }
-        j = lo;
+    const double g0 = a.grid[0];
+    int j = (int)floor((v - g0) * ((double)(a.n_psi - 1) / (a.grid[a.n_psi - 1] - g0)));
+    j = j < 0 ? 0 : (j > nm2 ? nm2 : j);
+    if (a.grid[j] <= v && (v < a.grid[j + 1] || j == nm2)) return j;
+    int lo = 0, hi = a.n_psi - 1;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.grid[mid] <= v)
+            lo = mid;
+        else
+            hi = mid;
     }
-    return j;
+    return lo;
 }
 
 struct DepoAcc {
@@ -208,134 +203,286 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
 #define TORJ_MIN_WAVES 2
 #endif
 
+// Per-lane ray state carried through a segment of steps.
+struct RayState {
+    double x[3], N[3], tau, Pdep;
+    int status, steps;
+};
+
+// Integrate one ray from its current step to `s_end` (the make_ray loop,
+// src/solve.jl:154-177): classic RK4 of sys!, optical depth, chunk-boundary
+// termination, shell deposition, trajectory samples.  Shared by the one-shot
+// and the work-queue kernels.
+template <bool ABS, bool DEPO, bool TRAJ>
+__device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w, RayState &r,
+                                            int s_end, AlbajarWork &work) {
+    const GLTable &gl = c_gl;
+    double *x = r.x, *N = r.N;
+    double tau = r.tau;
+    double P = exp(-tau);  // bitwise the value the previous step computed
+    double psi_a = 0.0;
+    DepoAcc dacc = {-1, 0.0};
+    if constexpr (DEPO) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+    const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
+    for (int s = r.steps; s < s_end; s++) {
+        // classic RK4 with a single RHS call site (one copy of the spline +
+        // Albajar code live -> lower VGPR pressure)
+        double acc[6] = {0, 0, 0, 0, 0, 0}, acc_a = 0.0, xt[3], Nt[3], k[6], al;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            xt[c] = x[c];
+            Nt[c] = N[c];
+        }
+#pragma unroll 1
+        for (int st = 0; st < 4; st++) {
+            ray_rhs<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, xt, Nt, k, al, &work);
+            const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
+            const double h = (st < 2) ? hds : ds;
+#pragma unroll
+            for (int c = 0; c < 6; c++) acc[c] = fma(wgt, k[c], acc[c]);
+            acc_a = fma(wgt, al, acc_a);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                xt[c] = fma(h, k[c], x[c]);
+                Nt[c] = fma(h, k[3 + c], N[c]);
+            }
+        }
+        double xn[3], Nn[3];
+        bool bad = false;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            xn[c] = x[c] + ds6 * acc[c];
+            Nn[c] = N[c] + ds6 * acc[3 + c];
+            bad |= !isfinite(xn[c]) || !isfinite(Nn[c]);
+        }
+        const double taun = tau + ds6 * acc_a;
+        bad |= !isfinite(taun);
+        if (bad) {
+            r.status = ST_NAN;
+            break;
+        }
+        const double Pn = exp(-taun);
+        const double dP = P - Pn;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = xn[c];
+            N[c] = Nn[c];
+        }
+        tau = taun;
+        P = Pn;
+        r.steps = s + 1;
+        const bool check = a.chunk_steps > 0 && (r.steps % a.chunk_steps) == 0;
+        double psi_b = 0.0;
+        if (DEPO || check) psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+        if constexpr (DEPO) {
+            r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
+            psi_a = psi_b;
+        }
+        if constexpr (TRAJ) {
+            if ((r.steps % a.traj_stride) == 0) {
+                const size_t si = (size_t)(r.steps / a.traj_stride - 1);
+                double *T = a.traj + si * 4 * (size_t)a.n + i;
+                T[0] = x[0];
+                T[(size_t)a.n] = x[1];
+                T[2 * (size_t)a.n] = x[2];
+                T[3 * (size_t)a.n] = tau;
+            }
+        }
+        if (check) {
+            if (psi_b > a.psi_exit) {  // src/solve.jl:174
+                r.status = ST_LEFT_PLASMA;
+                break;
+            }
+            if (P < a.P_min) {  // src/solve.jl:176
+                r.status = ST_ABSORBED;
+                break;
+            }
+        }
+    }
+    r.tau = tau;
+    if constexpr (DEPO) {
+        if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
+    }
+}
+
+__device__ __forceinline__ void load_start(const TraceArgs &a, int i, RayState &r) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        r.x[c] = a.x0[c * a.n + i];
+        r.N[c] = a.N0[c * a.n + i];
+    }
+    r.tau = 0.0;
+    r.Pdep = 0.0;
+    r.status = ST_OK;
+    r.steps = 0;
+}
+
+__device__ __forceinline__ void store_state(const TraceArgs &a, int i, const RayState &r) {
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        a.state[c * a.n + i] = r.x[c];
+        a.state[(3 + c) * a.n + i] = r.N[c];
+    }
+    a.state[6 * a.n + i] = r.tau;
+    a.status[i] = r.status;
+    a.steps[i] = r.steps;
+    if (a.Pdep) a.Pdep[i] = r.Pdep;
+}
+
+__device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long long steps,
+                                               const AlbajarWork &work) {
+    if (!a.counters) return;
+    const unsigned long long s0 = wave_sum(steps);
+    const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
+    const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
+    const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
+    if ((threadIdx.x & 63) == 0) {
+        atomicAdd(a.counters + 0, s0);
+        atomicAdd(a.counters + 1, 4ull * s0);
+        atomicAdd(a.counters + 2, s2);
+        atomicAdd(a.counters + 3, s3);
+        atomicAdd(a.counters + 4, s4);
+    }
+}
+
+// One-shot kernel: one lane per ray, all steps in one pass.
 template <bool ABS, bool DEPO, bool TRAJ>
 __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = i < a.n;
-    const GLTable &gl = c_gl;
     AlbajarWork work = {0u, 0u, 0u};
-    int steps = 0;
-    if (live) {
-        double x[3], N[3];
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            x[c] = a.x0[c * a.n + i];
-            N[c] = a.N0[c * a.n + i];
-        }
+    unsigned long long steps = 0;
+    if (i < a.n) {
+        RayState r;
+        load_start(a, i, r);
         const double w = (DEPO && a.w) ? a.w[i] : 1.0;
-        double tau = 0.0, P = 1.0;
-        int status = ST_OK;
-        double psi_a = 0.0;
-        DepoAcc dacc = {-1, 0.0};
-        double Pdep = 0.0;
-        if constexpr (DEPO) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
-        const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
-        for (int s = 0; s < a.n_steps; s++) {
-            // classic RK4 with a single RHS call site (keeps one copy of the
-            // spline + Albajar code live -> lower VGPR pressure)
-            double acc[6] = {0, 0, 0, 0, 0, 0}, acc_a = 0.0, xt[3], Nt[3], k[6], al;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                xt[c] = x[c];
-                Nt[c] = N[c];
+        ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, a.n_steps, work);
+        store_state(a, i, r);
+        if constexpr (DEPO) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
+        steps = r.steps;
+    }
+    flush_counters(a, steps, work);
+}
+
+// Work-queue kernel (ready-queue of ray groups).
+// The beam is cut into G groups of 64 rays (one wave each); a group's
+// integration is done in visits of `cs` steps (the reference's termination
+// chunk).  Waves pop a ready group, integrate one chunk, store its state and
+// push it back (or retire it when all its rays are done).  Groups therefore
+// migrate between SIMDs: SIMDs holding one wave (which runs a wave ~1.7x
+// faster than a SIMD holding two) absorb more visits, evening out the 1.53
+// waves/SIMD of a 1e5-ray beam.
+//
+// Queue: pops take head tickets h; h < G are the initial visits of group h;
+// h >= G consume push position p = h - G, published as one 8-byte granule
+// {tag = p + 1, group} (agent-scope release fence after the state stores, then
+// a relaxed agent store).  Pop: relaxed agent poll of the granule, then an
+// agent acquire fence before the state loads (MI355X_MICROARCH.md visibility
+// rules).  Every spin is bounded (err flag) and every wave exits once all G
+// groups have retired, so the grid always drains.
+struct SchedCtl {
+    unsigned head, tail, finished, err;
+};
+
+constexpr unsigned kGroupExit = 0xffffffffu;
+
+// returns the group index; bit 31 set = first visit (state from x0/N0)
+__device__ __forceinline__ unsigned sched_pop(SchedCtl *ctl, unsigned long long *slots, unsigned S,
+                                              unsigned G) {
+    unsigned g = kGroupExit;
+    if (threadIdx.x == 0) {
+        const unsigned h = __hip_atomic_fetch_add(&ctl->head, 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (h < G) {
+            g = h | 0x80000000u;
+        } else {
+            const unsigned long long pos = h - G;
+            unsigned long long *slot = slots + (pos % S);
+            for (unsigned spins = 0;; spins++) {
+                unsigned long long v = __hip_atomic_load(slot, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                if ((v >> 32) == pos + 1) {
+                    g = (unsigned)v;
+                    break;
+                }
+                if (__hip_atomic_load(&ctl->finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= G) {
+                    v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    g = ((v >> 32) == pos + 1) ? (unsigned)v : kGroupExit;
+                    break;
+                }
+                if (spins > (1u << 26)) {  // bounded spin: never hang the device
+                    __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(4);
             }
-#pragma unroll 1
-            for (int st = 0; st < 4; st++) {
-                ray_rhs<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, xt, Nt, k, al, &work);
-                const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
-                const double h = (st < 2) ? hds : ds;
-#pragma unroll
-                for (int c = 0; c < 6; c++) acc[c] = fma(wgt, k[c], acc[c]);
-                acc_a = fma(wgt, al, acc_a);
+        }
+    }
+    g = __shfl(g, 0, 64);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    return g;
+}
+
+__device__ __forceinline__ void sched_publish_begin() {
+    // every lane's state stores are issued by this one wave: drain them, then
+    // write back the XCD L2 (agent release) before the granule / counter
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool ABS, bool DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
+                                                                     unsigned long long *slots,
+                                                                     unsigned S, int G, int cs) {
+    AlbajarWork work = {0u, 0u, 0u};
+    unsigned long long steps = 0;
+    for (;;) {
+        const unsigned t = sched_pop(ctl, slots, S, (unsigned)G);
+        if (t == kGroupExit) break;
+        const unsigned g = t & 0x7fffffffu;
+        const int i = (int)g * 64 + threadIdx.x;
+        bool alive = false;
+        if (i < a.n) {
+            RayState r;
+            if (t & 0x80000000u) {
+                load_start(a, i, r);
+            } else {
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
-                    xt[c] = fma(h, k[c], x[c]);
-                    Nt[c] = fma(h, k[3 + c], N[c]);
+                    r.x[c] = a.state[c * a.n + i];
+                    r.N[c] = a.state[(3 + c) * a.n + i];
+                }
+                r.tau = a.state[6 * a.n + i];
+                r.status = a.status[i];
+                r.steps = a.steps[i];
+                r.Pdep = a.Pdep ? a.Pdep[i] : 0.0;
+            }
+            if (r.status == ST_OK && r.steps < a.n_steps) {
+                const int s0 = r.steps;
+                const int s_end = min(a.n_steps, (s0 / cs + 1) * cs);
+                const double w = (DEPO && a.w) ? a.w[i] : 1.0;
+                ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, s_end, work);
+                steps += (unsigned long long)(r.steps - s0);
+                alive = r.status == ST_OK && r.steps < a.n_steps;
+                if constexpr (DEPO) {
+                    if (!alive) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
                 }
             }
-            double xn[3], Nn[3];
-            bool bad = false;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                xn[c] = x[c] + ds6 * acc[c];
-                Nn[c] = N[c] + ds6 * acc[3 + c];
-                bad |= !isfinite(xn[c]) || !isfinite(Nn[c]);
-            }
-            const double taun = tau + ds6 * acc_a;
-            bad |= !isfinite(taun);
-            if (bad) {
-                status = ST_NAN;
-                break;
-            }
-            const double Pn = exp(-taun);
-            const double dP = P - Pn;
-#pragma unroll
-            for (int c = 0; c < 3; c++) {
-                x[c] = xn[c];
-                N[c] = Nn[c];
-            }
-            tau = taun;
-            P = Pn;
-            steps = s + 1;
-            const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
-            double psi_b = 0.0;
-            if (DEPO || check) psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
-            if constexpr (DEPO) {
-                Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
-                psi_a = psi_b;
-            }
-            if constexpr (TRAJ) {
-                if ((steps % a.traj_stride) == 0) {
-                    const size_t si = (size_t)(steps / a.traj_stride - 1);
-                    double *T = a.traj + si * 4 * (size_t)a.n + i;
-                    T[0] = x[0];
-                    T[(size_t)a.n] = x[1];
-                    T[2 * (size_t)a.n] = x[2];
-                    T[3 * (size_t)a.n] = tau;
-                }
-            }
-            if (check) {
-                if (psi_b > a.psi_exit) {  // src/solve.jl:174
-                    status = ST_LEFT_PLASMA;
-                    break;
-                }
-                if (P < a.P_min) {  // src/solve.jl:176
-                    status = ST_ABSORBED;
-                    break;
-                }
-            }
+            store_state(a, i, r);
         }
-        if constexpr (DEPO) {
-            if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
-            if (a.Pdep) a.Pdep[i] = Pdep;
-        }
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            a.state[c * a.n + i] = x[c];
-            a.state[(3 + c) * a.n + i] = N[c];
-        }
-        a.state[6 * a.n + i] = tau;
-        a.status[i] = status;
-        a.steps[i] = steps;
-        if constexpr (DEPO) {
-            // beam deposited power sum_rays w * P_dep(ray) in slot n_psi
-            double v = w * Pdep;
-            atomicAdd(a.dP + a.n_psi, v);
+        const bool any_alive = __any(alive);
+        sched_publish_begin();
+        if (threadIdx.x == 0) {
+            if (any_alive) {
+                const unsigned long long pos = __hip_atomic_fetch_add(&ctl->tail, 1u, __ATOMIC_RELAXED,
+                                                                      __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(slots + (pos % S), ((pos + 1) << 32) | (unsigned long long)g,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                __hip_atomic_fetch_add(&ctl->finished, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
     }
-    if (a.counters) {
-        const unsigned long long s0 = wave_sum((unsigned long long)steps);
-        const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
-        const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
-        const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(a.counters + 0, s0);
-            atomicAdd(a.counters + 1, 4ull * s0);
-            atomicAdd(a.counters + 2, s2);
-            atomicAdd(a.counters + 3, s3);
-            atomicAdd(a.counters + 4, s4);
-        }
-    }
+    flush_counters(a, steps, work);
 }
 
 struct EvalArgs {
@@ -538,6 +685,13 @@ struct torj_plasma_s {
     std::vector<double> vol_coef;
     double psi_prof_max = 0;
     hipStream_t stream = nullptr;
+    void *d_sched = nullptr;  // work-queue control block + ready-queue ring (zeroed per launch)
+    size_t sched_cap = 0;
+    bool last_sched = false;
+    int sched_mode = -1, sched_waves = 0;  // torj_set_sched  // last torj_trace_device launch used the work queue
+    double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
+    size_t ws_cap = 0;
+    int n_cu = 256;
     std::mutex mu;
 };
 
@@ -580,6 +734,29 @@ static int ensure_device(torj_plasma_s *p) {
     HIPCK(hipMemcpy(p->d_coef, p->coef.data(), p->coef.size() * sizeof(double),
                     hipMemcpyHostToDevice));
     HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
+    HIPCK(hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, p->device));
+    return 0;
+}
+
+static int ensure_sched(torj_plasma_s *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->sched_cap >= bytes) return 0;
+    if (p->d_sched) HIPCK(hipFree(p->d_sched));
+    p->d_sched = nullptr;
+    p->sched_cap = 0;
+    HIPCK(hipMalloc(&p->d_sched, bytes));
+    p->sched_cap = bytes;
+    return 0;
+}
+
+static int ensure_workspace(torj_plasma_s *p, size_t n) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->ws_cap >= n) return 0;
+    if (p->d_ws) HIPCK(hipFree(p->d_ws));
+    p->d_ws = nullptr;
+    p->ws_cap = 0;
+    HIPCK(hipMalloc(&p->d_ws, n * sizeof(double)));
+    p->ws_cap = n;
     return 0;
 }
 
@@ -940,6 +1117,8 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->d_coef) (void)hipSetDevice(p->device);
     if (p->d_coef) (void)hipFree(p->d_coef);
     if (p->stream) (void)hipStreamDestroy(p->stream);
+    if (p->d_sched) (void)hipFree(p->d_sched);
+    if (p->d_ws) (void)hipFree(p->d_ws);
     delete p;
     return 0;
 }
@@ -1252,18 +1431,13 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
     a.steps = steps;
     a.counters = (unsigned long long *)counters;
     if (depo) {
-        // host copy of the grid is not available here (device pointer): the
-        // uniform flag / spacing come from a small D2H read of the endpoints
-        double ends[2];
-        HIPCK(hipMemcpyAsync(&ends[0], grid, sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCK(hipMemcpyAsync(&ends[1], grid + n_psi - 1, sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCK(hipStreamSynchronize(s));
         a.n_psi = n_psi;
-        a.grid = grid;
-        a.g0 = ends[0];
-        a.ginv = (n_psi - 1) / (ends[1] - ends[0]);
-        a.grid_uniform = std::isfinite(a.ginv) && a.ginv > 0;  // index is corrected on the grid
+        a.grid = grid;  // uniform-grid fast path is set up in-kernel from grid[0], grid[n-1]
         a.dP = dP;
+        if (!Pdep) {  // the work-queue kernel carries P_dep across chunks: workspace
+            if (ensure_workspace(p, (size_t)n)) return -1;
+            Pdep = p->d_ws;
+        }
         a.Pdep = Pdep;
     }
     if (tr) {
@@ -1273,6 +1447,55 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
         if (a.n_save > 0)
             HIPCK(hipMemsetAsync(traj, 0xFF, (size_t)a.n_save * 4 * n * sizeof(double), s));  // NaN
     }
+    static const int sched_env = [] {
+        const char *e = getenv("TORJ_SCHED");
+        return e ? atoi(e) : 1;
+    }();
+    const int G = (n + 63) / 64;
+    const int cs = cfg->chunk_steps > 0 ? cfg->chunk_steps : std::max(cfg->n_steps, 1);
+    // default: the queue pays off once the beam exceeds one wave per SIMD
+    // (measured: 42k rays 111 vs 106 ms one-shot; 100k rays 151 vs 174 ms)
+    const int use_sched = p->sched_mode >= 0 ? p->sched_mode
+                                             : (sched_env && G > p->n_cu * 4 ? 1 : 0);
+    if (use_sched && cfg->n_steps > 0) {
+        // W persistent waves: at most 2 per SIMD (4 SIMDs per CU), and fewer
+        // than G so the ready queue keeps a backlog (a wave never waits for a
+        // group while another holds it); TORJ_SCHED_W overrides.
+        static const int w_env = [] {
+            const char *e = getenv("TORJ_SCHED_W");
+            return e ? atoi(e) : 0;
+        }();
+        int W = p->sched_waves > 0 ? p->sched_waves
+                : w_env > 0        ? w_env
+                                   : std::min(p->n_cu * 4 * 2, G - G / 16);
+        W = std::max(1, std::min(W, G));
+        const unsigned S = 4u * (unsigned)(G + W);  // ring slots (tag check makes reuse safe)
+        const size_t bytes = 256 + (size_t)S * sizeof(unsigned long long);
+        if (ensure_sched(p, bytes)) return -1;
+        HIPCK(hipMemsetAsync(p->d_sched, 0, bytes, s));
+        SchedCtl *ctl = (SchedCtl *)p->d_sched;
+        p->last_sched = true;
+        unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
+        const dim3 grd(W), blk(64);
+#define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace_sched<A, D, T>), grd, blk, 0, s, a, ctl, slots, S, G, cs)
+        if (cfg->absorption) {
+            if (depo) {
+                if (tr) LAUNCH(true, true, true); else LAUNCH(true, true, false);
+            } else {
+                if (tr) LAUNCH(true, false, true); else LAUNCH(true, false, false);
+            }
+        } else {
+            if (depo) {
+                if (tr) LAUNCH(false, true, true); else LAUNCH(false, true, false);
+            } else {
+                if (tr) LAUNCH(false, false, true); else LAUNCH(false, false, false);
+            }
+        }
+#undef LAUNCH
+        HIPCK(hipGetLastError());
+        return 0;
+    }
+    p->last_sched = false;
     const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
 #define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
     if (cfg->absorption) {
@@ -1290,6 +1513,15 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
     }
 #undef LAUNCH
     HIPCK(hipGetLastError());
+    return 0;
+}
+
+int torj_set_sched(torj_plasma_t p, int mode, int waves) {
+    if (!p) return fail("bad plasma handle");
+    if (mode < -1 || mode > 1) return fail("sched mode must be -1, 0 or 1");
+    if (waves < 0) return fail("waves must be >= 0");
+    p->sched_mode = mode;
+    p->sched_waves = waves;
     return 0;
 }
 
@@ -1341,6 +1573,13 @@ int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *
     }
     if (traj && n_save > 0 && ddownload(traj, dtraj, (size_t)n_save * 4 * n, s)) return -1;
     HIPCK(hipStreamSynchronize(s));
+    if (p->last_sched) {  // bounded-spin watchdog of the work queue
+        SchedCtl ctl;
+        HIPCK(hipMemcpy(&ctl, p->d_sched, sizeof(ctl), hipMemcpyDeviceToHost));
+        if (ctl.err) return fail("work-queue watchdog fired (ready-queue stalled)");
+        if (ctl.finished != (unsigned)((n + 63) / 64))
+            return fail("work queue retired %u of %d ray groups", ctl.finished, (n + 63) / 64);
+    }
     return 0;
 }
 

@@ -325,8 +325,8 @@ struct GLTable {
     double t[kMaxGL], w[kMaxGL], st[kMaxGL];  // nodes, weights, sqrt(1-t^2)
 };
 
-#ifndef TORJ_NODE_UNROLL
-#define TORJ_NODE_UNROLL 1
+#ifndef TORJ_ALBAJAR_NOINLINE
+#define TORJ_ALBAJAR_NOINLINE 1
 #endif
 
 // Horner evaluation of S_nu and S_{nu+1} at z with K terms; coefficients are
@@ -386,17 +386,65 @@ struct HarmConst {
 // S_m, S_{m+1} of K terms + the downward recurrence S_{m-1} = m S_m + z S_{m+1})
 // are computed once per pair.  With `single`, only the +t node is taken (the
 // middle node of an odd-order rule, t = 0).
+#ifndef TORJ_VGPR_COEFS
+#define TORJ_VGPR_COEFS 0
+#endif
+#ifndef TORJ_PAIR_UNROLL
+#define TORJ_PAIR_UNROLL 1
+#endif
+
+// Series coefficients of one harmonic for the node loop.  On the device they are
+// loaded once per harmonic into VGPRs (vector loads through an opaque zero lane
+// offset), so the Horner FMAs take register operands instead of 64-bit literals
+// re-materialised by two s_mov_b32 each per use.
 template <int M, int K>
-TORJ_HD double pair_term(const HarmConst &c, double t, double st, double w, bool single) {
+struct SeriesCoefs {
+    double a[K > 0 ? K : 1], b[K > 0 ? K : 1];
+    TORJ_HD void load() {
+        if constexpr (K > 0) {
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_VGPR_COEFS
+            int z;
+            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+            const double *ta = kSeriesTab.c[M - 2] + z, *tb = kSeriesTab.c[M - 1] + z;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                a[k] = ta[k];
+                b[k] = tb[k];
+            }
+#else
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+                a[k] = series_coef(M, k);
+                b[k] = series_coef(M + 1, k);
+            }
+#endif
+        }
+    }
+    TORJ_HD void eval(double z, double &Sa, double &Sb) const {
+        if constexpr (K > 0) {
+            double x = a[K - 1], y = b[K - 1];
+#pragma unroll
+            for (int k = K - 2; k >= 0; k--) {
+                x = fma(x, z, a[k]);
+                y = fma(y, z, b[k]);
+            }
+            Sa = x;
+            Sb = y;
+        } else {
+            series_pair_loop<M>(z, Sa, Sb);
+        }
+    }
+};
+
+template <int M, int K>
+TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
+                         double w, bool single) {
     constexpr double md = (double)M;
     const double arg = c.x_m * st;
     const double h = 0.5 * arg;
     const double h2 = h * h;
     double Sm, Sm1;
-    if constexpr (K > 0)
-        series_pair<K, M>(-h2, Sm, Sm1);
-    else
-        series_pair_loop<M>(-h2, Sm, Sm1);
+    sc.eval(-h2, Sm, Sm1);
     const double Sl = md * Sm - h2 * Sm1;
     double p = h;  // h^(2m-1)
 #pragma unroll
@@ -422,12 +470,28 @@ TORJ_HD double pair_term(const HarmConst &c, double t, double st, double w, bool
 
 template <int M, int K>
 TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
+    SeriesCoefs<M, K> sc;
+    sc.load();
     const int n = gl.n, half = n >> 1;
-    double acc = 0.0;
+    constexpr int U = TORJ_PAIR_UNROLL;
+    double acc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) acc[u] = 0.0;
+    int i = 0;
+    // U independent node pairs per iteration (ILP for the dependent fp64 chains)
 #pragma unroll 1
-    for (int i = 0; i < half; i++) acc += pair_term<M, K>(c, gl.t[i], gl.st[i], gl.w[i], false);
-    if (n & 1) acc += pair_term<M, K>(c, gl.t[half], gl.st[half], gl.w[half], true);
-    return acc;
+    for (; i + U <= half; i += U) {
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            acc[u] += pair_term<M, K>(c, sc, gl.t[i + u], gl.st[i + u], gl.w[i + u], false);
+    }
+#pragma unroll 1
+    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], false);
+    if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], true);
+    double s = acc[0];
+#pragma unroll
+    for (int u = 1; u < U; u++) s += acc[u];
+    return s;
 }
 
 struct AlbajarWork {
@@ -482,8 +546,15 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     return -mu * Pm * Pm * sum * sq_r;
 }
 
-// abs_Albajar_fast (src/absorption.jl:191-226)
-TORJ_HD double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
+// abs_Albajar_fast (src/absorption.jl:191-226).  With TORJ_ALBAJAR_NOINLINE the
+// device code keeps it out of line: the RK4 state is then saved once per call
+// instead of competing for registers inside the node loop.
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_ALBAJAR_NOINLINE
+#define TORJ_ALB_ATTR __host__ __device__ __attribute__((noinline))
+#else
+#define TORJ_ALB_ATTR TORJ_HD
+#endif
+TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
                                 double N_par, double Te, int mode, AlbajarWork *work) {
     if (Te < 20.0) return 0.0;
     const double mu = kMe * kC * kC / (kE * Te);

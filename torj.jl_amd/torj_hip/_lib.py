@@ -60,6 +60,7 @@ _SIGS = {
                                  _dp, _ip]),
     "torj_trace": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                              _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
+    "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

@@ -93,6 +93,10 @@ class Plasma:
         check(lib().torj_plasma_volume(self._h, len(p), dptr(p), dptr(out)))
         return out if np.ndim(psi) else float(out[0])
 
+    def set_sched(self, mode: int = -1, waves: int = 0):
+        """torj_set_sched: -1 default, 0 one lane per ray, 1 ready-queue waves."""
+        check(lib().torj_set_sched(self._h, int(mode), int(waves)))
+
     def shell_volumes(self, psi_grid):
         g = f64(psi_grid)
         dV = np.zeros(max(len(g) - 1, 0))
