@@ -165,6 +165,10 @@ def main():
     if rank == 0:
         status = d_status.cpu().numpy()
         flop = F.algorithmic_flops(cnt, n_gl=24)
+        n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
+        sched = os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd
+        kname = "k_trace_sched<1,1,1>" if sched else "k_trace<1,1,1>"
+        traffic = measured_traffic(kname, n, args)
         kern_s = float(km.item()) / 1e3
         achieved = flop / kern_s / 1e12
         out = {
@@ -188,6 +192,8 @@ def main():
                             f"n_psi={args.n_psi}, traj stride {args.traj_stride}",
                 "rays_per_gpu": n,
                 "rk4_steps": args.n_steps,
+                "n_psi": args.n_psi,
+                "traj_stride": args.traj_stride,
                 "parallelism": f"ray-shard x{world} + RCCL all_reduce of dP/dV",
                 "ray_status_counts": {T.STATUS_NAMES[i]: int(c)
                                       for i, c in enumerate(np.bincount(status, minlength=6)) if c},
@@ -198,8 +204,9 @@ def main():
                 "peak": FP64_VECTOR_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
-                "traffic": None,
-                "kernel": "k_trace<ABS,DEPO,TRAJ>",
+                "traffic": traffic["traffic_bytes"] if traffic else None,
+                "traffic_source": traffic["file"] if traffic else None,
+                "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
                 "algorithmic_flop_per_launch": flop,
                 "flop_per_ray_step": flop / max(cnt[0], 1),
@@ -213,6 +220,28 @@ def main():
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def measured_traffic(kname, n, args):
+    """HBM bytes per launch of the hot kernel, measured offline by
+    scripts/profile.sh (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950
+    correction) and summarised by tools/prof_summary.py into
+    profiles/<round>/traffic.json; used only if it was taken on this workload
+    and kernel (PMC collection cannot run inside the timed process)."""
+    import glob
+    base = kname.split("<")[0] + "<"
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+        try:
+            t = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        wl = t.get("workload", {})
+        if (base in (t.get("kernel") or "") and wl.get("rays") == n
+                and wl.get("rk4_steps") == args.n_steps and wl.get("n_psi") == args.n_psi
+                and wl.get("traj_stride") == args.traj_stride):
+            t["file"] = os.path.relpath(f, ROOT)
+            return t
+    return None
 
 
 def cpu_baseline(eq, xp, Np, w, omega, args, grid):

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh output directory into profiles/<round>/.
+
+usage: python tools/prof_summary.py gpurun_out/<tag> profiles/r01 [kernel-substring]
+       (the workload is read from the JSON line of <tag>/trace.log)
+
+Writes
+  kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
+  pmc_summary.json   per-dispatch averages of every PMC counter of the hot kernel
+  traffic.json       HBM traffic per launch of the hot kernel, from FETCH_SIZE /
+                     WRITE_SIZE (KiB) with the gfx950 correction of
+                     MI355X_MICROARCH.md "HBM": FETCH_SIZE x 2
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+
+def workload(src):
+    try:
+        for line in open(os.path.join(src, "trace.log")):
+            if line.startswith("{"):
+                d = json.loads(line)
+                c = d["config"]
+                return {"rays": c["rays_per_gpu"], "rk4_steps": c["rk4_steps"],
+                        "n_psi": c.get("n_psi"), "traj_stride": c.get("traj_stride"),
+                        "kernel_ms_bench": d["roofline"]["kernel_ms"]}
+    except (OSError, ValueError, KeyError):
+        pass
+    return {}
+
+
+def main():
+    src, dst = sys.argv[1], sys.argv[2]
+    key = sys.argv[3] if len(sys.argv) > 3 else "k_trace"
+    os.makedirs(dst, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
+    hot = None
+    if stats:
+        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+        for r in csv.DictReader(open(stats[0])):
+            if key in r["Name"] and (hot is None or float(r["TotalDurationNs"]) > hot[2]):
+                hot = (r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]))
+    vals = defaultdict(list)
+    meta = {}
+    for f in sorted(glob.glob(os.path.join(src, "pmc*", "*counter_collection.csv"))):
+        for r in csv.DictReader(open(f)):
+            if key not in r["Kernel_Name"]:
+                continue
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            meta = {k: r[k] for k in ("Kernel_Name", "Grid_Size", "Workgroup_Size", "Scratch_Size",
+                                      "VGPR_Count", "Accum_VGPR_Count", "SGPR_Count", "LDS_Block_Size")}
+    pmc = {k: sum(v) / len(v) for k, v in sorted(vals.items())}
+    out = {"kernel": meta, "dispatches_per_counter": {k: len(v) for k, v in vals.items()}, "avg": pmc}
+    if hot:
+        out["kernel_stats"] = {"name": hot[0], "calls": hot[1], "avg_ns": hot[3]}
+    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
+        fetch = 2.0 * pmc["FETCH_SIZE"] * 1024.0  # KiB, half-counted on gfx950
+        write = pmc["WRITE_SIZE"] * 1024.0
+        tr = {"kernel": meta.get("Kernel_Name"), "fetch_bytes": fetch, "write_bytes": write,
+              "traffic_bytes": fetch + write,
+              "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, per-dispatch "
+                        "average; FETCH_SIZE x2 (gfx950), KiB -> bytes",
+              "source": os.path.basename(os.path.normpath(src)), "workload": workload(src)}
+        json.dump(tr, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+        print(json.dumps(tr))
+    if hot:
+        print(f"{hot[0]}: {hot[1]} calls, avg {hot[3] / 1e6:.2f} ms")
+
+
+if __name__ == "__main__":
+    main()
