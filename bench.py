@@ -215,11 +215,35 @@ def main():
                               "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
                               "bessel_series_terms": int(cnt[4])},
         }
+        if world == 1:
+            out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps):
+    """PCIe-inclusive rate of the host-pointer boundary (torj_trace: device
+    allocation, H2D of the start states, the trace, D2H of state, status,
+    steps, dP_shell, P_dep and the trajectory).  Reported beside `value`,
+    never as it."""
+    n = len(w)
+    xs, Ns = np.ascontiguousarray(xp.T), np.ascontiguousarray(Np.T)
+    state, status, steps = np.zeros((7, n)), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    dP, Pdep = np.zeros(len(grid) + 1), np.zeros(n)
+    traj = np.zeros((max(n_save, 1), 4, n))
+    dp, ip = T._lib.dptr, T._lib.iptr
+    t0 = time.perf_counter()
+    T._lib.check(T.lib().torj_trace(plasma.handle, cfg, n, dp(xs), dp(Ns), dp(w), len(grid), dp(grid),
+                                    dp(state), ip(status), ip(steps), dp(dP), dp(Pdep),
+                                    dp(traj) if n_save else None))
+    dt = time.perf_counter() - t0
+    return {"value": ray_steps / dt, "unit": "ray-steps/s", "ms": dt * 1e3,
+            "d2h_bytes": int(state.nbytes + status.nbytes + steps.nbytes + dP.nbytes + Pdep.nbytes
+                             + (traj.nbytes if n_save else 0)),
+            "note": "torj_trace host-pointer path incl. PCIe transfers (not the headline)"}
 
 
 def measured_traffic(kname, n, args):
