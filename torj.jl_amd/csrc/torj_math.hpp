@@ -436,6 +436,51 @@ struct SeriesCoefs {
     }
 };
 
+// Node-loop elementary functions.  On the device: sqrt of a normal positive
+// argument from v_rsq_f64 + one Goldschmidt step + one Newton correction
+// (~1 ulp; the library sequence adds a second correction for correct rounding
+// plus denormal scaling and class checks), and exp of a non-positive argument
+// (range reduction + degree-12 Taylor, ~1 ulp; no overflow path; underflows to
+// 0 through ldexp).  Arguments here: 1 + u^2 >= 1 and mu (1 - gamma) <= 0.
+#ifndef TORJ_FAST_NODE_MATH
+#define TORJ_FAST_NODE_MATH 1
+#endif
+TORJ_HD double sqrt_pos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    return fma(fma(-g, g, x), h, g);
+#else
+    return sqrt(x);
+#endif
+}
+TORJ_HD double exp_nonpos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+    const double k = __builtin_rint(x * 1.4426950408889634074);
+    double r = fma(-k, 6.93147180559945286227e-01, x);
+    r = fma(-k, 2.31904681384629955842e-17, r);
+    double p = 1.0 / 479001600.0;  // 1/12!
+    p = fma(p, r, 1.0 / 39916800.0);
+    p = fma(p, r, 1.0 / 3628800.0);
+    p = fma(p, r, 1.0 / 362880.0);
+    p = fma(p, r, 1.0 / 40320.0);
+    p = fma(p, r, 1.0 / 5040.0);
+    p = fma(p, r, 1.0 / 720.0);
+    p = fma(p, r, 1.0 / 120.0);
+    p = fma(p, r, 1.0 / 24.0);
+    p = fma(p, r, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    return __builtin_amdgcn_ldexp(p, (int)fmax(k, -2000.0));
+#else
+    return exp(x);
+#endif
+}
+
 template <int M, int K>
 TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
                          double w, bool single) {
@@ -457,13 +502,13 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double
     // +t
     const double brp = A * fma(t, fma(c.K3, t, c.K4), c.K0) - B + Cc * fma(c.K5, t, c.K1);
     const double upp = fma(c.upa1, t, c.upa0);
-    const double gp = sqrt(fma(upp, upp, u_perp1));
-    double r = (wp * brp) * exp(c.mu * (1.0 - gp));
+    const double gp = sqrt_pos(fma(upp, upp, u_perp1));
+    double r = (wp * brp) * exp_nonpos(c.mu * (1.0 - gp));
     if (!single) {  // -t
         const double brm = A * fma(-t, fma(-c.K3, t, c.K4), c.K0) - B + Cc * fma(-c.K5, t, c.K1);
         const double upm = fma(-c.upa1, t, c.upa0);
-        const double gm = sqrt(fma(upm, upm, u_perp1));
-        r += (wp * brm) * exp(c.mu * (1.0 - gm));
+        const double gm = sqrt_pos(fma(upm, upm, u_perp1));
+        r += (wp * brm) * exp_nonpos(c.mu * (1.0 - gm));
     }
     return r;
 }
@@ -478,15 +523,33 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = 0.0;
     int i = 0;
-    // U independent node pairs per iteration (ILP for the dependent fp64 chains)
+    if constexpr (U > 1) {
+        // U independent node pairs per iteration (ILP for the dependent fp64 chains)
 #pragma unroll 1
-    for (; i + U <= half; i += U) {
+        for (; i + U <= half; i += U) {
 #pragma unroll
-        for (int u = 0; u < U; u++)
-            acc[u] += pair_term<M, K>(c, sc, gl.t[i + u], gl.st[i + u], gl.w[i + u], false);
+            for (int u = 0; u < U; u++)
+                acc[u] += pair_term<M, K>(c, sc, gl.t[i + u], gl.st[i + u], gl.w[i + u], false);
+        }
     }
+    // remaining pairs, with the (uniform, scalar-loaded) node constants of pair
+    // i+1 fetched while pair i computes (gl arrays hold kMaxGL > half entries)
+    double tn = gl.t[i], sn = gl.st[i], wn = gl.w[i];
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], false);
+    for (; i < half; i++) {
+        const double t = tn, st = sn, w = wn;
+        tn = gl.t[i + 1];
+        sn = gl.st[i + 1];
+        wn = gl.w[i + 1];
+        const double r = pair_term<M, K>(c, sc, t, st, w, false);
+#ifdef __HIP_DEVICE_COMPILE__
+        // consume the prefetched constants at the END of the iteration, so the
+        // s_load latency hides behind this pair (otherwise load PRE re-rolls
+        // them to the loop head, right before their first use)
+        asm volatile("" : "+s"(tn), "+s"(sn), "+s"(wn));
+#endif
+        acc[0] += r;
+    }
     if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], true);
     double s = acc[0];
 #pragma unroll
