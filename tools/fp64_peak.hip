@@ -39,8 +39,9 @@ void run(int waves_per_simd, double *d) {
 int main() {
     double *d;
     hipMalloc(&d, 4096);
-    for (int w : {1, 2, 4, 8}) run<1>(w, d);
-    for (int w : {1, 2, 4, 8}) run<4>(w, d);
+    for (int w : {1, 2, 3, 4, 8}) run<1>(w, d);
+    for (int w : {1, 2, 3, 4}) run<2>(w, d);
+    for (int w : {1, 2, 3, 4, 8}) run<4>(w, d);
     for (int w : {1, 2, 4, 8}) run<8>(w, d);
     return 0;
 }

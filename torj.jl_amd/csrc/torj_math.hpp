@@ -445,6 +445,9 @@ struct SeriesCoefs {
 #ifndef TORJ_FAST_NODE_MATH
 #define TORJ_FAST_NODE_MATH 1
 #endif
+#ifndef TORJ_EXP_ESTRIN
+#define TORJ_EXP_ESTRIN 0
+#endif
 TORJ_HD double sqrt_pos(double x) {
 #if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
     const double y = __builtin_amdgcn_rsq(x);
@@ -462,6 +465,17 @@ TORJ_HD double exp_nonpos(double x) {
     const double k = __builtin_rint(x * 1.4426950408889634074);
     double r = fma(-k, 6.93147180559945286227e-01, x);
     r = fma(-k, 2.31904681384629955842e-17, r);
+#if TORJ_EXP_ESTRIN
+    // Estrin form: depth 5 instead of 12 (more independent work per wave)
+    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
+    const double a0 = fma(r, 1.0, 1.0), a1 = fma(r, 1.0 / 6.0, 0.5);
+    const double a2 = fma(r, 1.0 / 120.0, 1.0 / 24.0), a3 = fma(r, 1.0 / 5040.0, 1.0 / 720.0);
+    const double a4 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0);
+    const double a5 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0);
+    const double b0 = fma(r2, a1, a0), b1 = fma(r2, a3, a2), b2 = fma(r2, a5, a4);
+    const double c1 = fma(r4, 1.0 / 479001600.0, b2);
+    const double p = fma(r8, c1, fma(r4, b1, b0));
+#else
     double p = 1.0 / 479001600.0;  // 1/12!
     p = fma(p, r, 1.0 / 39916800.0);
     p = fma(p, r, 1.0 / 3628800.0);
@@ -475,6 +489,7 @@ TORJ_HD double exp_nonpos(double x) {
     p = fma(p, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
+#endif
     return __builtin_amdgcn_ldexp(p, (int)fmax(k, -2000.0));
 #else
     return exp(x);
@@ -522,34 +537,45 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
     double acc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = 0.0;
-    int i = 0;
-    if constexpr (U > 1) {
-        // U independent node pairs per iteration (ILP for the dependent fp64 chains)
-#pragma unroll 1
-        for (; i + U <= half; i += U) {
+    // U independent node pairs per iteration (ILP for the dependent fp64
+    // chains), with the (uniform, scalar-loaded) node constants of the next U
+    // pairs fetched while these compute (gl arrays hold kMaxGL >= half + U
+    // entries, so the look-ahead never leaves the table)
+    double tn[U], sn[U], wn[U];
 #pragma unroll
-            for (int u = 0; u < U; u++)
-                acc[u] += pair_term<M, K>(c, sc, gl.t[i + u], gl.st[i + u], gl.w[i + u], false);
-        }
+    for (int u = 0; u < U; u++) {
+        tn[u] = gl.t[u];
+        sn[u] = gl.st[u];
+        wn[u] = gl.w[u];
     }
-    // remaining pairs, with the (uniform, scalar-loaded) node constants of pair
-    // i+1 fetched while pair i computes (gl arrays hold kMaxGL > half entries)
-    double tn = gl.t[i], sn = gl.st[i], wn = gl.w[i];
+    int i = 0;
 #pragma unroll 1
-    for (; i < half; i++) {
-        const double t = tn, st = sn, w = wn;
-        tn = gl.t[i + 1];
-        sn = gl.st[i + 1];
-        wn = gl.w[i + 1];
-        const double r = pair_term<M, K>(c, sc, t, st, w, false);
+    for (; i + U <= half; i += U) {
+        double t[U], st[U], w[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            t[u] = tn[u];
+            st[u] = sn[u];
+            w[u] = wn[u];
+            tn[u] = gl.t[i + U + u];
+            sn[u] = gl.st[i + U + u];
+            wn[u] = gl.w[i + U + u];
+        }
+        double r[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) r[u] = pair_term<M, K>(c, sc, t[u], st[u], w[u], false);
 #ifdef __HIP_DEVICE_COMPILE__
         // consume the prefetched constants at the END of the iteration, so the
-        // s_load latency hides behind this pair (otherwise load PRE re-rolls
+        // s_load latency hides behind these pairs (otherwise load PRE re-rolls
         // them to the loop head, right before their first use)
-        asm volatile("" : "+s"(tn), "+s"(sn), "+s"(wn));
+#pragma unroll
+        for (int u = 0; u < U; u++) asm volatile("" : "+s"(tn[u]), "+s"(sn[u]), "+s"(wn[u]));
 #endif
-        acc[0] += r;
+#pragma unroll
+        for (int u = 0; u < U; u++) acc[u] += r[u];
     }
+#pragma unroll 1
+    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], false);
     if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], true);
     double s = acc[0];
 #pragma unroll
