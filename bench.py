@@ -87,7 +87,9 @@ def main():
     phi = 2 * np.pi * rank / max(world, 1)  # weak scaling: each rank its own (rotated) beam
     rot = np.array([[np.cos(phi), -np.sin(phi), 0], [np.sin(phi), np.cos(phi), 0], [0, 0, 1]])
     pos, dirs = pos @ rot.T, dirs @ rot.T
-    xp, Np, s0, st = T.ray_entry(plasma, pos, dirs, omega, args.mode)
+    t_entry = time.perf_counter()
+    xp, Np, s0, st = T.ray_entry(plasma, pos, dirs, omega, args.mode, gpu=True)
+    t_entry = time.perf_counter() - t_entry  # first call: includes device setup
     if not (st == 0).all():
         raise RuntimeError(f"ray entry failed for {(st != 0).sum()} rays")
     n = len(w)
@@ -217,6 +219,7 @@ def main():
         }
         if world == 1:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local)
+            out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
         print(json.dumps(out), flush=True)
@@ -244,6 +247,19 @@ def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps):
             "d2h_bytes": int(state.nbytes + status.nbytes + steps.nbytes + dP.nbytes + Pdep.nbytes
                              + (traj.nbytes if n_save else 0)),
             "note": "torj_trace host-pointer path incl. PCIe transfers (not the headline)"}
+
+
+def entry_timing(T, plasma, pos, dirs, omega, mode, t_first):
+    """first_point + vacuum_plasma_refraction for the whole beam (setup, outside
+    `value`): the GPU kernel through the host-pointer ABI, vs the host C++ path."""
+    t0 = time.perf_counter()
+    T.ray_entry(plasma, pos, dirs, omega, mode, gpu=True)
+    t_gpu = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    T.ray_entry(plasma, pos, dirs, omega, mode)
+    t_host = time.perf_counter() - t0
+    return {"gpu_ms": t_gpu * 1e3, "gpu_first_call_ms": t_first * 1e3, "host_ms": t_host * 1e3,
+            "host_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())}
 
 
 def measured_traffic(kname, n, args):

@@ -129,6 +129,15 @@ int torj_launch_peripheral_rays(const double x0[3], const double N0[3], double w
  * point, refracted N, vacuum path length s0 and a status per ray. */
 int torj_ray_entry(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
                    int mode, double *x_plasma, double *N_plasma, double *s0, int *status);
+/* Same computation on the GPU (one lane per ray), device pointers, async on
+ * `stream` (hipStream_t or NULL).  Replaces the per-ray host bisection + NLsolve
+ * of make_beam's ray loop (src/solve.jl:219-221 -> :137-141). */
+int torj_ray_entry_device(torj_plasma_t p, int n, const double *x0, const double *N0,
+                          double omega, int mode, double *x_plasma, double *N_plasma, double *s0,
+                          int *status, void *stream);
+/* Host pointers, GPU compute (upload, torj_ray_entry_device, download). */
+int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
+                       int mode, double *x_plasma, double *N_plasma, double *s0, int *status);
 
 /* ---- the hot path: ray stepping (src/solve.jl:144-177) ------------------- */
 typedef struct {

@@ -162,6 +162,37 @@ def test_trace_matches_oracle_2000_steps(gpu, T, hplasma, oplasma, fan_states, m
         assert np.median(g.P_end) < 0.05  # X2 absorption happens on this path
 
 
+def test_gpu_ray_entry_matches_host_and_oracle(gpu, T, hplasma, oplasma, eq):
+    """first_point + vacuum_plasma_refraction as a HIP kernel (torj_ray_entry_gpu)
+    vs the host C++ path and the oracle: launch fan incl. off-grid launch points
+    (toroidal intersection), both modes, and the REFLECTED status."""
+    from torj_hip import synthetic as S
+
+    om = 2 * np.pi * 92.5e9
+    N0 = T.pol_tor_angles_2_vector(np.deg2rad(30), 0.0)
+    pos, dirs, w = T.launch_peripheral_rays([2.5, 0, 0.4], N0, 0.0174, 1 / 3.99, 92.5e9,
+                                            N_rings=8, min_azimuthal_points=7)
+    extra_p = np.array([[2.9, 0.0, 0.2], [2.0, 0.0, 1.2], [2.9, 0.3, 0.0]])
+    extra_d = np.array([[-1.0, 0.0, -0.1], [0.05, 0.0, -1.0], [-1.0, -0.05, 0.02]])
+    extra_d /= np.linalg.norm(extra_d, axis=1)[:, None]
+    pos, dirs = np.vstack([pos, extra_p]), np.vstack([dirs, extra_d])
+    for mode in (1, -1):
+        g = T.ray_entry(hplasma, pos, dirs, om, mode, gpu=True)
+        h = T.ray_entry(hplasma, pos, dirs, om, mode)
+        assert np.array_equal(g[3], h[3])
+        ok = g[3] == T.OK
+        assert ok.sum() >= len(pos) - 1
+        for a, b in zip(g[:3], h[:3]):
+            assert np.abs(a[ok] - b[ok]).max() < 1e-12
+        for i in np.flatnonzero(ok)[::5]:
+            so, xo, No, s0o = oplasma.ray_entry(pos[i], dirs[i], om, mode)
+            assert so == 0
+            assert np.abs(g[0][i] - xo).max() < 1e-12 and np.abs(g[1][i] - No).max() < 1e-12
+            assert abs(g[2][i] - s0o) < 1e-12
+    dense = T.Plasma(*S.plasma_args(S.circular_tokamak(ne_edge=3e20)))
+    assert T.ray_entry(dense, [[2.5, 0, 0.4]], [N0], om, -1, gpu=True)[3][0] == T.REFLECTED
+
+
 @pytest.mark.parametrize("waves", [1, 3, 0])
 def test_trace_independent_of_scheduling(gpu, T, hplasma, fan_states, waves):
     """The ready-queue kernel (groups migrate between waves chunk by chunk; 1 and

@@ -27,6 +27,7 @@
 
 #include "../../include/torj_hip.h"
 #include "torj_math.hpp"
+#include "torj_entry.hpp"
 
 using namespace torj;
 
@@ -485,6 +486,37 @@ __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a,
     flush_counters(a, steps, work);
 }
 
+// ---------------------------------------------------------------------------
+// GPU ray entry (src/solve.jl:7-74): one lane per ray.  The bisection to the
+// psi_prof_max surface runs ~55 spline evaluations per lane; lanes of a wave
+// take nearly the same number, so 64-lane blocks keep divergence low.
+// ---------------------------------------------------------------------------
+struct EntryArgs {
+    const double *coef;
+    Grid g;
+    double psi_max, omega;
+    int mode, n;
+    const double *x0, *N0;
+    double *xp, *Np, *s0;
+    int *status;
+};
+
+__global__ void __launch_bounds__(64) k_ray_entry(EntryArgs a) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const double x0[3] = {a.x0[i], a.x0[a.n + i], a.x0[2 * a.n + i]};
+    const double N0[3] = {a.N0[i], a.N0[a.n + i], a.N0[2 * a.n + i]};
+    double xo[3], No[3], s0;
+    const int st = ray_entry_one(a.coef, a.g, a.psi_max, x0, N0, a.omega, a.mode, xo, No, s0);
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        a.xp[k * a.n + i] = xo[k];
+        a.Np[k * a.n + i] = No[k];
+    }
+    a.s0[i] = s0;
+    a.status[i] = st;
+}
+
 struct EvalArgs {
     const double *coef;
     Grid g;
@@ -758,162 +790,6 @@ static int ensure_workspace(torj_plasma_s *p, size_t n) {
     HIPCK(hipMalloc(&p->d_ws, n * sizeof(double)));
     p->ws_cap = n;
     return 0;
-}
-
-// ===========================================================================
-// host ray entry: first_point + vacuum_plasma_refraction (src/solve.jl:7-74)
-// ===========================================================================
-static double host_psi(const torj_plasma_s *p, const double x[3]) {
-    return eval_one(p->coef.data(), p->g, std::hypot(x[0], x[1]), x[2], F_PSI);
-}
-
-// IMAS.toroidal_intersection for the grid rectangle (src/solve.jl:22-24):
-// smallest t > 0 at which p0 + t v meets the surface of revolution of the
-// polygon (R_k, Z_k).  Parity unpinned (IMAS not available).
-static double toroidal_intersection(const double *Rp, const double *Zp, int np, const double p0[3],
-                                    const double v[3]) {
-    double best = INFINITY;
-    for (int s = 0; s + 1 < np; s++) {
-        const double Ra = Rp[s], Za = Zp[s], Rb = Rp[s + 1], Zb = Zp[s + 1];
-        if (Zb == Za) {
-            if (v[2] == 0.0) continue;
-            const double t = (Za - p0[2]) / v[2];
-            if (!(t > 0)) continue;
-            const double R = std::hypot(p0[0] + t * v[0], p0[1] + t * v[1]);
-            if (R >= std::min(Ra, Rb) && R <= std::max(Ra, Rb)) best = std::min(best, t);
-            continue;
-        }
-        // R(t)^2 = (al + be t)^2 on the cone through the segment
-        const double k = (Rb - Ra) / (Zb - Za);
-        const double al = Ra + (p0[2] - Za) * k, be = v[2] * k;
-        const double A = v[0] * v[0] + v[1] * v[1] - be * be;
-        const double B = 2.0 * (p0[0] * v[0] + p0[1] * v[1] - al * be);
-        const double C = p0[0] * p0[0] + p0[1] * p0[1] - al * al;
-        double ts[2];
-        int nt = 0;
-        if (std::fabs(A) < 1e-300) {
-            if (B != 0) ts[nt++] = -C / B;
-        } else {
-            const double disc = B * B - 4 * A * C;
-            if (disc >= 0) {
-                const double sq = std::sqrt(disc);
-                ts[nt++] = (-B - sq) / (2 * A);
-                ts[nt++] = (-B + sq) / (2 * A);
-            }
-        }
-        for (int q = 0; q < nt; q++) {
-            const double t = ts[q];
-            if (!(t > 0)) continue;
-            const double sp = (p0[2] + t * v[2] - Za) / (Zb - Za);
-            if (sp < 0 || sp > 1 || al + be * t < 0) continue;
-            best = std::min(best, t);
-        }
-    }
-    return best;
-}
-
-static int host_first_point(const torj_plasma_s *p, const double x0[3], const double N0[3],
-                            double out[3]) {
-    const Grid &g = p->g;
-    double pp[3] = {x0[0], x0[1], x0[2]};
-    const double R0 = std::hypot(x0[0], x0[1]);
-    const bool on_grid = g.R1 <= R0 && R0 <= g.Rn && g.Z1 <= x0[2] && x0[2] <= g.Zn;  // :7-11
-    if (!on_grid) {
-        const double Rp[5] = {g.R1, g.Rn, g.Rn, g.R1, g.R1};
-        const double Zp[5] = {g.Z1, g.Z1, g.Zn, g.Zn, g.Z1};
-        const double t = toroidal_intersection(Rp, Zp, 5, x0, N0);
-        if (!std::isfinite(t)) return ST_ENTRY_FAIL;
-        for (int k = 0; k < 3; k++) pp[k] = x0[k] + N0[k] * t;
-    }
-    auto G = [&](double t) {
-        const double q[3] = {pp[0] + t * N0[0], pp[1] + t * N0[1], pp[2] + t * N0[2]};
-        return host_psi(p, q) - p->psi_prof_max;
-    };
-    // find_zero(g, (0, 0.5), Bisection()) (:29), bisected to machine precision
-    double a = 0.0, b = 0.5, ga = G(a), gb = G(b);
-    if (ga != 0.0 && gb != 0.0) {
-        if ((ga > 0) == (gb > 0)) return ST_ENTRY_FAIL;
-        for (int it = 0; it < 200; it++) {
-            const double m = 0.5 * (a + b);
-            if (m <= a || m >= b) break;
-            const double gm = G(m);
-            if (gm == 0.0) {
-                a = b = m;
-                ga = gb = 0.0;
-                break;
-            }
-            if ((gm > 0) == (ga > 0)) {
-                a = m;
-                ga = gm;
-            } else {
-                b = m;
-                gb = gm;
-            }
-        }
-    }
-    const double t = (std::fabs(ga) <= std::fabs(gb)) ? a : b;
-    for (int k = 0; k < 3; k++) pp[k] += t * N0[k];
-    const double psi_ref = host_psi(p, pp);
-    if (!(std::fabs(psi_ref - p->psi_prof_max) < 1e-6)) return ST_ENTRY_FAIL;  // :32
-    if (psi_ref > p->psi_prof_max)                                              // :33-36
-        for (int k = 0; k < 3; k++) pp[k] += 2.0 * (psi_ref - p->psi_prof_max) * N0[k];
-    for (int k = 0; k < 3; k++) out[k] = pp[k];
-    return ST_OK;
-}
-
-static void host_eval_plasma(const torj_plasma_s *p, const double x[3], const double N[3],
-                             double omega, double &X, double &Y, double &Npar, double b[3]) {
-    PlasmaPoint pt;
-    plasma_point<false>(p->coef.data(), p->g, make_consts(omega), x, pt);
-    X = pt.X;
-    Y = pt.Y;
-    for (int k = 0; k < 3; k++) b[k] = pt.b[k];
-    Npar = N[0] * b[0] + N[1] * b[1] + N[2] * b[2];
-}
-
-// The 3 refraction equations (:40-49) have the root N = n0 + (cos_i -
-// sqrt(q^2 - sin_i^2)) n with q^2 = N_s^2(N.b): solved as a scalar equation in q.
-static int host_refraction(const torj_plasma_s *p, const double pp[3], const double N0[3],
-                           double omega, int mode, double N[3]) {
-    double X, Y, Npar, b[3];
-    host_eval_plasma(p, pp, N0, omega, X, Y, Npar, b);
-    const double Nest = refractive_index_sq(X, Y, 0.0, mode);
-    if (Nest <= 0) return ST_REFLECTED;  // :57-59
-    double q = std::sqrt(Nest);
-    const double R = std::hypot(pp[0], pp[1]);
-    double v, dR, dZ;
-    eval_grad_one(p->coef.data(), p->g, R, pp[2], F_PSI, v, dR, dZ);
-    double n[3] = {dR * pp[0] / R, dR * pp[1] / R, dZ};
-    const double nn = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-    for (double &c : n) c /= nn;
-    const double n0n = std::sqrt(N0[0] * N0[0] + N0[1] * N0[1] + N0[2] * N0[2]);
-    const double n0[3] = {N0[0] / n0n, N0[1] / n0n, N0[2] / n0n};
-    const double ci = -(n[0] * n0[0] + n[1] * n0[1] + n[2] * n0[2]);
-    const double si2 = 1.0 - ci * ci;
-    const double nb = n[0] * b[0] + n[1] * b[1] + n[2] * b[2];
-    const double n0b = n0[0] * b[0] + n0[1] * b[1] + n0[2] * b[2];
-    auto resid = [&](double qq, bool &ok) {
-        const double rt = qq * qq - si2;
-        ok = rt >= 0;
-        if (!ok) return 0.0;
-        const double np = n0b + (ci - std::sqrt(rt)) * nb;
-        return qq * qq - refractive_index_sq(X, Y, np, mode);
-    };
-    for (int it = 0; it < 100; it++) {
-        bool ok;
-        const double r = resid(q, ok);
-        if (!ok) return ST_REFLECTED;
-        const double h = 1e-7 * q;
-        bool o1, o2;
-        const double dr = (resid(q + h, o1) - resid(q - h, o2)) / (2 * h);
-        if (!o1 || !o2 || !(dr != 0)) return ST_ENTRY_FAIL;
-        const double dq = r / dr;
-        q -= dq;
-        if (std::fabs(dq) <= 1e-16 * q) break;
-    }
-    const double s = std::sqrt(q * q - si2);
-    for (int k = 0; k < 3; k++) N[k] = n0[k] + (ci - s) * n[k];
-    return ST_OK;
 }
 
 // ===========================================================================
@@ -1222,31 +1098,22 @@ int torj_launch_peripheral_rays(const double x0[3], const double N0[3], double w
 int torj_ray_entry(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
                    int mode, double *xp, double *Np, double *s0, int *status) {
     if (!p) return fail("bad plasma handle");
+    if (mode != 1 && mode != -1) return fail("mode must be +1 (X) or -1 (O)");
+    const double *coef = p->coef.data();
 #pragma omp parallel for schedule(dynamic, 16)
     for (int i = 0; i < n; i++) {
         const double a[3] = {x0[i], x0[(size_t)n + i], x0[2 * (size_t)n + i]};
         const double d[3] = {N0[i], N0[(size_t)n + i], N0[2 * (size_t)n + i]};
-        double xo[3] = {NAN, NAN, NAN}, No[3] = {NAN, NAN, NAN};
-        int st = host_first_point(p, a, d, xo);
-        if (st == ST_OK && !(host_psi(p, xo) <= p->psi_prof_max)) st = ST_ENTRY_FAIL;  // :138
-        if (st == ST_OK) st = host_refraction(p, xo, d, omega, mode, No);
-        if (st == ST_OK) {  // :141 |D| < 1e-12
-            double X, Y, Npar, b[3];
-            host_eval_plasma(p, xo, No, omega, X, Y, Npar, b);
-            const double D = No[0] * No[0] + No[1] * No[1] + No[2] * No[2] -
-                             refractive_index_sq(X, Y, Npar, mode);
-            if (!(std::fabs(D) < 1e-12)) st = ST_ENTRY_FAIL;
-        }
+        double xo[3], No[3];
+        status[i] = ray_entry_one(coef, p->g, p->psi_prof_max, a, d, omega, mode, xo, No, s0[i]);
         for (int k = 0; k < 3; k++) {
             xp[(size_t)k * n + i] = xo[k];
             Np[(size_t)k * n + i] = No[k];
         }
-        s0[i] = std::sqrt((xo[0] - a[0]) * (xo[0] - a[0]) + (xo[1] - a[1]) * (xo[1] - a[1]) +
-                          (xo[2] - a[2]) * (xo[2] - a[2]));
-        status[i] = st;
     }
     return 0;
 }
+
 
 }  // extern "C"
 
@@ -1394,6 +1261,41 @@ int torj_abs_albajar_fast(int n, const double *omega, const double *X, const dou
 int torj_refractive_index_sq(int n, const double *X, const double *Y, const double *Npar, int mode,
                              double *out) {
     return batched_scalar(false, n, nullptr, X, Y, nullptr, Npar, nullptr, mode, out);
+}
+
+int torj_ray_entry_device(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
+                          int mode, double *xp, double *Np, double *s0, int *status, void *stream) {
+    if (!p) return fail("bad plasma handle");
+    if (mode != 1 && mode != -1) return fail("mode must be +1 (X) or -1 (O)");
+    if (n <= 0) return 0;
+    if (ensure_device(p)) return -1;
+    EntryArgs a{p->d_coef, p->g, p->psi_prof_max, omega, mode, n, x0, N0, xp, Np, s0, status};
+    hipLaunchKernelGGL(k_ray_entry, dim3(nblocks(n, 64)), dim3(64), 0, (hipStream_t)stream, a);
+    HIPCK(hipGetLastError());
+    return 0;
+}
+
+int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N0, double omega,
+                       int mode, double *xp, double *Np, double *s0, int *status) {
+    if (!p) return fail("bad plasma handle");
+    if (n <= 0) return 0;
+    if (ensure_device(p)) return -1;
+    hipStream_t s = p->stream;
+    DevBufs B;
+    double *dx0, *dN0, *dxp, *dNp, *ds0;
+    int *dst;
+    if (dupload(&dx0, x0, 3 * (size_t)n, s) || dupload(&dN0, N0, 3 * (size_t)n, s)) return -1;
+    B.track(dx0), B.track(dN0);
+    if (dalloc(&dxp, 3 * (size_t)n, true) || dalloc(&dNp, 3 * (size_t)n, true) ||
+        dalloc(&ds0, n, true) || dalloc(&dst, n, true))
+        return -1;
+    B.track(dxp), B.track(dNp), B.track(ds0), B.track(dst);
+    if (torj_ray_entry_device(p, n, dx0, dN0, omega, mode, dxp, dNp, ds0, dst, s)) return -1;
+    if (ddownload(xp, dxp, 3 * (size_t)n, s) || ddownload(Np, dNp, 3 * (size_t)n, s) ||
+        ddownload(s0, ds0, n, s) || ddownload(status, dst, n, s))
+        return -1;
+    HIPCK(hipStreamSynchronize(s));
+    return 0;
 }
 
 int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,

@@ -58,6 +58,11 @@ _SIGS = {
                                               C.c_int, C.c_int, C.c_int, _ip, _dp, _dp, _dp]),
     "torj_ray_entry": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_double, C.c_int, _dp, _dp,
                                  _dp, _ip]),
+    "torj_ray_entry_device": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_double,
+                                        C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                        C.c_void_p]),
+    "torj_ray_entry_gpu": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_double, C.c_int, _dp,
+                                     _dp, _dp, _ip]),
     "torj_trace": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                              _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),

@@ -24,16 +24,19 @@ class RayEntryError(AssertionError):
     and its unhandled reflection return (src/solve.jl:57-59)."""
 
 
-def ray_entry(plasma, x0, N0, omega: float, mode: int):
+def ray_entry(plasma, x0, N0, omega: float, mode: int, *, gpu: bool = False):
     """first_point + vacuum_plasma_refraction for a batch (src/solve.jl:7-74).
-    Returns (x_plasma (n,3), N_plasma (n,3), s0 (n,), status (n,))."""
+    Returns (x_plasma (n,3), N_plasma (n,3), s0 (n,), status (n,)).  gpu=True
+    runs the one-lane-per-ray HIP kernel (torj_ray_entry_gpu); the default is
+    the host C++ path (OpenMP), usable without a GPU."""
     xs, Ns = soa(x0), soa(N0)
     n = xs.shape[1]
     xp, Np = np.zeros((3, n)), np.zeros((3, n))
     s0 = np.zeros(n)
     st = np.zeros(n, dtype=np.int32)
-    check(lib().torj_ray_entry(plasma.handle, n, dptr(xs), dptr(Ns), float(omega), int(mode),
-                               dptr(xp), dptr(Np), dptr(s0), iptr(st)))
+    fn = lib().torj_ray_entry_gpu if gpu else lib().torj_ray_entry
+    check(fn(plasma.handle, n, dptr(xs), dptr(Ns), float(omega), int(mode), dptr(xp), dptr(Np),
+             dptr(s0), iptr(st)))
     return xp.T.copy(), Np.T.copy(), s0, st
 
 
@@ -113,7 +116,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     N0 = pol_tor_angles_2_vector(steering_angle_pol, steering_angle_tor)
     x0 = np.array([r * np.cos(phi), r * np.sin(phi), z])
     pos, dirs, w = launch_peripheral_rays(x0, N0, spot_size, inverse_curvature_radius, f, **kwargs)
-    xp, Np, s0, st = ray_entry(plasma, pos, dirs, omega, mode)
+    xp, Np, s0, st = ray_entry(plasma, pos, dirs, omega, mode, gpu=True)
     bad = np.flatnonzero(st != OK)
     if len(bad):
         raise RayEntryError(f"{len(bad)} rays failed entry, first: ray {bad[0]} "
