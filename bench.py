@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--freq", type=float, default=92.5e9)
     ap.add_argument("--n-psi", type=int, default=1000)
     ap.add_argument("--traj-stride", type=int, default=100)
+    ap.add_argument("--deposition", choices=["binned", "reference"], default="reference",
+                    help="binned: in-kernel psi-shell binning; reference: "
+                         "power_deposition_profile's FITPACK semantics (extra kernel)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
@@ -107,18 +110,20 @@ def main():
     n_save = args.n_steps // args.traj_stride if args.traj_stride > 0 else 0
     d_traj = torch.empty((max(n_save, 1), 4, n), dtype=torch.float64, device=dev)
     d_cnt = torch.zeros(5, dtype=torch.int64, device=dev)
+    dep = 1 if args.deposition == "reference" else 0
     cfg = T._lib.TraceCfg(omega, args.mode, args.ds, args.n_steps, max(1, args.n_steps // 100),
-                          1.0, 1e-6, 1, args.traj_stride)
+                          1.0, 1e-6, 1, args.traj_stride, dep)
+    d_xl, d_s0 = dev_t(pos.T), dev_t(s0)
     L = T.lib()
     stream = torch.cuda.current_stream(dev)
 
     def launch(counters=None):
         d_dP.zero_()
-        T._lib.check(L.torj_trace_device(
+        T._lib.check(L.torj_trace_device_ex(
             plasma.handle, cfg, n, d_x0.data_ptr(), d_N0.data_ptr(), d_w.data_ptr(), args.n_psi,
-            d_grid.data_ptr(), d_state.data_ptr(), d_status.data_ptr(), d_steps.data_ptr(),
-            d_dP.data_ptr(), d_Pdep.data_ptr(), d_traj.data_ptr() if n_save else None,
-            counters, stream.cuda_stream))
+            d_grid.data_ptr(), d_xl.data_ptr(), d_s0.data_ptr(), d_state.data_ptr(),
+            d_status.data_ptr(), d_steps.data_ptr(), d_dP.data_ptr(), d_Pdep.data_ptr(),
+            d_traj.data_ptr() if n_save else None, counters, stream.cuda_stream))
 
     def one_step(ev=None):
         if ev is not None:
@@ -191,7 +196,7 @@ def main():
                 "workload": f"C3: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
                             f"min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, {args.n_steps} RK4 "
                             f"steps ds={args.ds:g} m, Albajar alpha (GL-24), psi-shell deposition "
-                            f"n_psi={args.n_psi}, traj stride {args.traj_stride}",
+                            f"n_psi={args.n_psi} ({args.deposition}), traj stride {args.traj_stride}",
                 "rays_per_gpu": n,
                 "rk4_steps": args.n_steps,
                 "n_psi": args.n_psi,
@@ -218,7 +223,8 @@ def main():
                               "bessel_series_terms": int(cnt[4])},
         }
         if world == 1:
-            out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local)
+            out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,
+                                            pos, s0)
             out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
@@ -227,7 +233,7 @@ def main():
         dist.destroy_process_group()
 
 
-def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps):
+def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps, pos, s0):
     """PCIe-inclusive rate of the host-pointer boundary (torj_trace: device
     allocation, H2D of the start states, the trace, D2H of state, status,
     steps, dP_shell, P_dep and the trajectory).  Reported beside `value`,
@@ -239,9 +245,10 @@ def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps):
     traj = np.zeros((max(n_save, 1), 4, n))
     dp, ip = T._lib.dptr, T._lib.iptr
     t0 = time.perf_counter()
-    T._lib.check(T.lib().torj_trace(plasma.handle, cfg, n, dp(xs), dp(Ns), dp(w), len(grid), dp(grid),
-                                    dp(state), ip(status), ip(steps), dp(dP), dp(Pdep),
-                                    dp(traj) if n_save else None))
+    xl = np.ascontiguousarray(pos.T)
+    T._lib.check(T.lib().torj_trace_ex(plasma.handle, cfg, n, dp(xs), dp(Ns), dp(w), len(grid),
+                                       dp(grid), dp(xl), dp(s0), dp(state), ip(status), ip(steps),
+                                       dp(dP), dp(Pdep), dp(traj) if n_save else None))
     dt = time.perf_counter() - t0
     return {"value": ray_steps / dt, "unit": "ray-steps/s", "ms": dt * 1e3,
             "d2h_bytes": int(state.nbytes + status.nbytes + steps.nbytes + dP.nbytes + Pdep.nbytes

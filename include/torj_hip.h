@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 1
+#define TORJ_ABI_VERSION 2
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -150,6 +150,11 @@ typedef struct {
     double P_min;     /* 1e-6 in the reference (src/solve.jl:176) */
     int absorption;   /* 1: integrate optical depth with abs_Albajar_fast */
     int traj_stride;  /* 0: no trajectory; else save (x,y,z,tau) every traj_stride steps */
+    int deposition;   /* 0: in-kernel psi-shell binning of the RK4 steps (fast, default);
+                         1: the reference's power_deposition_profile (src/plasma.jl:91-151):
+                            not-a-knot cubic splines of psi(s) and dP/ds = P alpha through
+                            make_ray's saved points, boundary roots paired per shell,
+                            |integral| per pair, outside-in walk -- needs torj_trace_ex */
 } torj_trace_cfg;
 
 /* Host-pointer form.  x0, N0: in-plasma start states (3 x n); weights (n, may
@@ -166,6 +171,16 @@ int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *
                double *state, int *status, int *steps, double *dP_shell, double *P_dep,
                double *traj);
 
+/* With the vacuum launch points x_launch (3 x n, make_ray's first point, s = 0)
+ * and path lengths s0 (n) to the entry point -- what cfg->deposition = 1 needs
+ * to rebuild make_ray's s / psi vectors.  With deposition = 1, dP_shell[j] is
+ * sum_rays w dP_j of the reference profile, dP_shell[n_psi] = sum_rays w P and
+ * P_dep[i] = the ray's deposited power P (src/plasma.jl:140-147). */
+int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                  const double *N0, const double *weights, int n_psi, const double *psi_grid,
+                  const double *x_launch, const double *s0, double *state, int *status,
+                  int *steps, double *dP_shell, double *P_dep, double *traj);
+
 /* Device-pointer form (inputs resident in HBM; what bench.py times).
  * dP_shell (n_psi+1) is ACCUMULATED into (zero it first).  counters (may be
  * NULL): 5 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
@@ -176,6 +191,11 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
                       const double *psi_grid, double *state, int *status, int *steps,
                       double *dP_shell, double *P_dep, double *traj, uint64_t *counters,
                       void *stream);
+int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                         const double *N0, const double *weights, int n_psi,
+                         const double *psi_grid, const double *x_launch, const double *s0,
+                         double *state, int *status, int *steps, double *dP_shell, double *P_dep,
+                         double *traj, uint64_t *counters, void *stream);
 
 /* Scheduling of torj_trace / torj_trace_device launches on this plasma handle
  * (no reference counterpart: an MI355X tuning knob; results are independent

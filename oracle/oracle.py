@@ -177,8 +177,10 @@ class OraclePlasma:
 
     def trace(self, x0, N0, omega, mode, ds, n_steps, chunk_steps=None, psi_exit=1.0,
               P_min=1e-6, absorption=True, psi_grid=None, weights=None, traj_stride=0,
-              n_threads=None):
-        """Fixed-step RK4 trace of rays (x0, N0: (n, 3) entry states)."""
+              n_threads=None, samples=False):
+        """Fixed-step RK4 trace of rays (x0, N0: (n, 3) entry states).  samples=True
+        adds "samples": (n, n_steps+1, 2) = (psi_k, dP/ds_k) at the entry point and
+        every step (make_ray's psi / dP_ds vectors, src/solve.jl:151,171)."""
         x0, N0 = _c(x0).reshape(-1, 3), _c(N0).reshape(-1, 3)
         n = x0.shape[0]
         if chunk_steps is None:
@@ -196,11 +198,16 @@ class OraclePlasma:
         traj = np.full((n, max(n_save, 1), 4), np.nan)
         w = _c(weights) if weights is not None else None
         nt = n_threads or default_threads()
-        lib().or_trace(self.ref, C.byref(cfg), n, _p(x0), _p(N0), _p(w) if w is not None else None,
-                       _p(state), status.ctypes.data_as(_ip), steps.ctypes.data_as(_ip), _p(dP),
-                       _p(Pdep), _p(traj), nt)
-        return dict(state=state, status=status, steps=steps, dP=dP[:n_psi], Pdep=Pdep,
-                    traj=traj[:, :n_save])
+        smp = np.zeros((n, n_steps + 1, 2)) if samples else None
+        lib().or_trace_samples(self.ref, C.byref(cfg), n, _p(x0), _p(N0),
+                               _p(w) if w is not None else None, _p(state),
+                               status.ctypes.data_as(_ip), steps.ctypes.data_as(_ip), _p(dP),
+                               _p(Pdep), _p(traj), _p(smp) if samples else None, nt)
+        out = dict(state=state, status=status, steps=steps, dP=dP[:n_psi], Pdep=Pdep,
+                   traj=traj[:, :n_save])
+        if samples:
+            out["samples"] = smp
+        return out
 
 
 class _TraceCfg(C.Structure):

@@ -1174,6 +1174,14 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
              const double *N0, const double *weights, double *out_state, int *out_status,
              int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
              int n_threads) {
+    return or_trace_samples(p, cfg, n_rays, x0, N0, weights, out_state, out_status, out_steps,
+                            out_dP, out_Pdep, out_traj, NULL, n_threads);
+}
+
+int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
+                     const double *N0, const double *weights, double *out_state, int *out_status,
+                     int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
+                     double *out_samples, int n_threads) {
     const double ds = cfg->ds;
     const int n_psi = cfg->n_psi;
     int n_save = cfg->traj_stride > 0 ? cfg->n_steps / cfg->traj_stride : 0;
@@ -1199,6 +1207,12 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
         int status = OR_OK, steps = 0;
         double psi_a = (n_psi > 0) ? or_evaluate(&p->psi, u) : 0.0;
         double Pdep = 0.0;
+        double *smp = out_samples ? out_samples + (size_t)r * (cfg->n_steps + 1) * 2 : NULL;
+        if (smp) {
+            for (int k = 0; k < 2 * (cfg->n_steps + 1); k++) smp[k] = NAN;
+            smp[0] = or_evaluate(&p->psi, u);
+            smp[1] = 0.0;
+        }
         for (int s = 0; s < cfg->n_steps; s++) {
             double k1[6], k2[6], k3[6], k4[6], a1, a2, a3, a4, ut[6];
             rhs(p, u, cfg->omega, cfg->mode, cfg->absorption, k1, &a1);
@@ -1225,6 +1239,12 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
             tau = taun;
             steps = s + 1;
             double psi_b = or_evaluate(&p->psi, u);
+            if (smp) { /* dP_ds = P alpha_approx at the saved point (src/solve.jl:171) */
+                smp[2 * steps] = psi_b;
+                smp[2 * steps + 1] =
+                    cfg->absorption ? exp(-tau) * or_alpha_approx(p, u, u + 3, cfg->omega, cfg->mode)
+                                    : 0.0;
+            }
             if (n_psi > 0) {
                 Pdep += deposit(cfg->psi_grid, n_psi, psi_a, psi_b, dP, w, acc);
                 psi_a = psi_b;

@@ -144,6 +144,15 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
              int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
              int n_threads);
 
+/* Same, plus the per-step samples make_ray stores for power_deposition_profile
+ * (src/solve.jl:164-172): out_samples n_rays x (n_steps+1) x 2 =
+ * (psi(x_k), dP/ds_k = P_k alpha_approx(x_k, N_k)) for k = 0 (entry point,
+ * dP/ds = 0 as the reference's initial vector, :151) .. steps; NaN beyond. */
+int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
+                     const double *N0, const double *weights, double *out_state, int *out_status,
+                     int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
+                     double *out_samples, int n_threads);
+
 #ifdef __cplusplus
 }
 #endif

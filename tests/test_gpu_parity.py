@@ -308,7 +308,8 @@ def test_make_ray_matches_oracle(gpu, T, hplasma, oplasma):
     N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
     x0 = [s["R0"], 0.0, s["z0"]]
     grid = np.linspace(0, 1, 1000)
-    sv, u, P_beam, dP_dV, pdep = T.make_ray(hplasma, x0, N0, s["f"], 1, 0.4, grid)
+    sv, u, P_beam, dP_dV, pdep = T.make_ray(hplasma, x0, N0, s["f"], 1, 0.4, grid,
+                                            deposition="binned")
     assert len(sv) == len(u) == len(P_beam) == 4002
     assert np.all(np.diff(sv) > 0) and sv[0] == 0.0
     om = 2 * np.pi * s["f"]

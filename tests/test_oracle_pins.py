@@ -316,3 +316,45 @@ def test_rk4_fourth_order(O, oplasma):
     e2 = np.linalg.norm(ends[1] - ends[3])
     e3 = np.linalg.norm(ends[2] - ends[3])
     assert 8 < e1 / e2 < 24 or 8 < e2 / e3 < 24
+
+
+def test_deposition_ref_pinned_on_analytic_profile():
+    """oracle/deposition_ref.py (power_deposition_profile on scipy's FITPACK) on
+    an analytic ray: psi(s) = 1 - 1.6 s (1 - s) dips to 0.6 at s = 0.5 and comes
+    back, dP/ds Gaussian.  Exact shell powers come from the exact boundary
+    crossings and scipy.integrate.quad; the spline-interpolated profile must
+    agree to the interpolation error of 2 000 samples, the shells inside the
+    ray's deepest point are 0 (the outside-in break), and a ray that ends
+    inside the plasma drops its last, unpaired root (odd count)."""
+    import deposition_ref as D
+    from scipy.integrate import quad
+
+    psi = lambda s: 1.0 - 1.6 * s * (1.0 - s)
+    dpds = lambda s: np.exp(-((s - 0.3) / 0.08) ** 2)
+    s_in = lambda L: 0.5 * (1 - np.sqrt(max(1 - 4 * (1 - L) / 1.6, 0.0)))  # psi(s_in) = L, s < 0.5
+    grid = np.linspace(0.0, 1.0, 41)
+    s = np.linspace(0.0, 1.0, 2001)
+
+    def exact(s_end):
+        out = np.zeros(len(grid))
+        for k in range(len(grid) - 1):
+            lo, hi = grid[k], grid[k + 1]
+            if hi <= 0.6:
+                continue
+            a, b = s_in(hi), s_in(max(lo, 0.6))
+            segs = [(a, b), (1 - b, 1 - a)]
+            tot = sum(quad(dpds, x, min(y, s_end), epsabs=1e-15)[0] for x, y in segs if y <= s_end)
+            out[k] = tot / (hi - lo)
+        return out
+
+    prof, P = D.power_deposition_profile(s, psi(s), dpds(s), grid, lambda p: p)  # V(psi) = psi
+    ex = exact(1.0)
+    assert np.abs(prof - ex).max() <= 1e-8 * np.abs(ex).max()
+    assert np.all(prof[:-1][grid[1:] <= 0.6] == 0.0)
+    assert abs(P - quad(dpds, 0.0, 1.0, epsabs=1e-15)[0]) <= 1e-8
+    # ending at s = 0.8 (psi = 0.744): the shell it ends in has an odd root count,
+    # its partial second crossing is dropped; shells crossed completely twice are kept
+    m = s <= 0.8 + 1e-12
+    prof2, _ = D.power_deposition_profile(s[m], psi(s[m]), dpds(s[m]), grid, lambda p: p)
+    ex2 = exact(0.8)
+    assert np.abs(prof2 - ex2).max() <= 1e-8 * np.abs(ex).max()

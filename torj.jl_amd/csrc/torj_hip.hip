@@ -28,6 +28,7 @@
 #include "../../include/torj_hip.h"
 #include "torj_math.hpp"
 #include "torj_entry.hpp"
+#include "torj_fitdepo.hpp"
 
 using namespace torj;
 
@@ -128,7 +129,12 @@ struct TraceArgs {
     int n_save;
     double *traj;  // n_save x 4 x n
     unsigned long long *counters;
+    double *smp_psi;   // DEPO == 2: psi(x_k), (n_steps + 1) x n
+    double *smp_dpds;  // DEPO == 2: P_k alpha(x_k), (n_steps + 1) x n
 };
+
+// DEPO modes of the trace kernels
+constexpr int kDepoNone = 0, kDepoBinned = 1, kDepoSamples = 2;
 
 // psi shell j with grid[j] <= v < grid[j+1], clamped to [0, n-2]; identical
 // result to a binary search on the grid array.
@@ -214,7 +220,7 @@ struct RayState {
 // src/solve.jl:154-177): classic RK4 of sys!, optical depth, chunk-boundary
 // termination, shell deposition, trajectory samples.  Shared by the one-shot
 // and the work-queue kernels.
-template <bool ABS, bool DEPO, bool TRAJ>
+template <bool ABS, int DEPO, bool TRAJ>
 __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w, RayState &r,
                                             int s_end, AlbajarWork &work) {
     const GLTable &gl = c_gl;
@@ -223,12 +229,18 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
     double P = exp(-tau);  // bitwise the value the previous step computed
     double psi_a = 0.0;
     DepoAcc dacc = {-1, 0.0};
-    if constexpr (DEPO) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+    if constexpr (DEPO != kDepoNone) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+    if constexpr (DEPO == kDepoSamples) {
+        if (r.steps == 0) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
+            a.smp_psi[i] = psi_a;
+            a.smp_dpds[i] = 0.0;
+        }
+    }
     const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
     for (int s = r.steps; s < s_end; s++) {
         // classic RK4 with a single RHS call site (one copy of the spline +
         // Albajar code live -> lower VGPR pressure)
-        double acc[6] = {0, 0, 0, 0, 0, 0}, acc_a = 0.0, xt[3], Nt[3], k[6], al;
+        double acc[6] = {0, 0, 0, 0, 0, 0}, acc_a = 0.0, xt[3], Nt[3], k[6], al, al0 = 0.0;
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             xt[c] = x[c];
@@ -242,6 +254,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
 #pragma unroll
             for (int c = 0; c < 6; c++) acc[c] = fma(wgt, k[c], acc[c]);
             acc_a = fma(wgt, al, acc_a);
+            if constexpr (DEPO == kDepoSamples) al0 = (st == 0) ? al : al0;
 #pragma unroll
             for (int c = 0; c < 3; c++) {
                 xt[c] = fma(h, k[c], x[c]);
@@ -264,6 +277,11 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         }
         const double Pn = exp(-taun);
         const double dP = P - Pn;
+        if constexpr (DEPO == kDepoSamples) {
+            // dP/ds at the saved point x_s = P_s alpha_approx(x_s) (src/solve.jl:171):
+            // the stage-0 RHS of this step evaluated exactly that alpha (al0)
+            if (s > 0) a.smp_dpds[(size_t)s * a.n + i] = P * al0;
+        }
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             x[c] = xn[c];
@@ -274,8 +292,10 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         r.steps = s + 1;
         const bool check = a.chunk_steps > 0 && (r.steps % a.chunk_steps) == 0;
         double psi_b = 0.0;
-        if (DEPO || check) psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
-        if constexpr (DEPO) {
+        if (DEPO != kDepoNone || check)
+            psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+        if constexpr (DEPO == kDepoSamples) a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
+        if constexpr (DEPO == kDepoBinned) {
             r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
             psi_a = psi_b;
         }
@@ -301,7 +321,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         }
     }
     r.tau = tau;
-    if constexpr (DEPO) {
+    if constexpr (DEPO == kDepoBinned) {
         if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
     }
 }
@@ -347,7 +367,7 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
 }
 
 // One-shot kernel: one lane per ray, all steps in one pass.
-template <bool ABS, bool DEPO, bool TRAJ>
+template <bool ABS, int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     AlbajarWork work = {0u, 0u, 0u};
@@ -355,10 +375,10 @@ __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs 
     if (i < a.n) {
         RayState r;
         load_start(a, i, r);
-        const double w = (DEPO && a.w) ? a.w[i] : 1.0;
+        const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
         ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, a.n_steps, work);
         store_state(a, i, r);
-        if constexpr (DEPO) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
+        if constexpr (DEPO == kDepoBinned) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
         steps = r.steps;
     }
     flush_counters(a, steps, work);
@@ -430,7 +450,7 @@ __device__ __forceinline__ void sched_publish_begin() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool ABS, bool DEPO, bool TRAJ>
+template <bool ABS, int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
                                                                      unsigned long long *slots,
                                                                      unsigned S, int G, int cs) {
@@ -460,11 +480,11 @@ __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a,
             if (r.status == ST_OK && r.steps < a.n_steps) {
                 const int s0 = r.steps;
                 const int s_end = min(a.n_steps, (s0 / cs + 1) * cs);
-                const double w = (DEPO && a.w) ? a.w[i] : 1.0;
+                const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
                 ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, s_end, work);
                 steps += (unsigned long long)(r.steps - s0);
                 alive = r.status == ST_OK && r.steps < a.n_steps;
-                if constexpr (DEPO) {
+                if constexpr (DEPO == kDepoBinned) {
                     if (!alive) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
                 }
             }
@@ -515,6 +535,93 @@ __global__ void __launch_bounds__(64) k_ray_entry(EntryArgs a) {
     }
     a.s0[i] = s0;
     a.status[i] = st;
+}
+
+// dP/ds at a ray's last saved point (every other point's alpha is the next
+// step's stage-0 RHS inside the trace kernel): P alpha_approx(x, N) from the
+// final state (src/solve.jl:171)
+template <bool ABS>
+__global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const int k = a.steps[i];
+    if (k <= 0) return;
+    double x[3], N[3], du[6], al = 0.0;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        x[c] = a.state[c * a.n + i];
+        N[c] = a.state[(3 + c) * a.n + i];
+    }
+    if constexpr (ABS) ray_rhs<true>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, x, N, du, al, nullptr);
+    a.smp_dpds[(size_t)k * a.n + i] = exp(-a.state[6 * a.n + i]) * al;
+}
+
+// ---------------------------------------------------------------------------
+// Reference-faithful deposition (torj_fitdepo.hpp): one lane per ray
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(64) k_fit_depo(FitArgs a) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const int m = a.steps[i] + 2;  // launch point, entry point, one per step
+    if (m < 4 || !(a.s0[i] > 0.0)) {  // FITPACK needs > k = 3 strictly increasing points
+        a.kstar[i] = a.n_psi;  // no shell counts
+        a.Pray[i] = 0.0;
+        return;
+    }
+    const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
+    RayData R{&a, i, m, a.s0[i], psi_at(a.coef, a.g, xl)};
+    nak_solve(R);
+    Walker W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    walk_ray(W, R);
+    // the reference's outside-in walk stops at the first shell whose two
+    // boundaries have < 2 roots together (src/plasma.jl:120-124)
+    int kstar = -1;
+    const size_t n = a.n;
+    for (int k0 = a.n_psi - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
+        int cv[kChunk + 1];
+#pragma unroll
+        for (int u = 0; u <= kChunk; u++) cv[u] = a.cnt[(size_t)max(k0 - u + 1, 0) * n + i];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {  // shell k = k0 - u: boundaries k and k + 1
+            const int k = k0 - u;
+            if (k >= 0 && kstar < 0 && cv[u + 1] + cv[u] < 2) kstar = k;
+        }
+    }
+    a.kstar[i] = kstar;
+    double P = 0.0;
+    for (int q0 = a.n_psi - 2; q0 > kstar; q0 -= kChunk) {
+        double v[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) v[u] = a.dPs[(size_t)max(q0 - u, 0) * n + i];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++)
+            if (q0 - u > kstar) P += v[u];
+    }
+    a.Pray[i] = P;
+}
+
+// make_beam's sums over rays (src/solve.jl:236-239), atomic-free per shell:
+// dP[k] += sum_i w_i dP_k(ray i) over rays whose outside-in walk reached k;
+// block n_psi - 1 sums w_i P_i into dP[n_psi].
+__global__ void __launch_bounds__(256) k_shell_sum(FitArgs a) {
+    const int k = blockIdx.x;
+    double acc = 0.0;
+    if (k < a.n_psi - 1) {
+        const double *row = a.dPs + (size_t)k * a.n;
+        for (int i = threadIdx.x; i < a.n; i += 256)
+            if (k > a.kstar[i]) acc += (a.w ? a.w[i] : 1.0) * row[i];
+    } else {
+        for (int i = threadIdx.x; i < a.n; i += 256) acc += (a.w ? a.w[i] : 1.0) * a.Pray[i];
+    }
+    __shared__ double red[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = (red[0] + red[1]) + (red[2] + red[3]);
+        a.dP[k < a.n_psi - 1 ? k : a.n_psi] += t;
+    }
 }
 
 struct EvalArgs {
@@ -719,8 +826,10 @@ struct torj_plasma_s {
     hipStream_t stream = nullptr;
     void *d_sched = nullptr;  // work-queue control block + ready-queue ring (zeroed per launch)
     size_t sched_cap = 0;
-    bool last_sched = false;
-    int sched_mode = -1, sched_waves = 0;  // torj_set_sched  // last torj_trace_device launch used the work queue
+    bool last_sched = false;               // last torj_trace_device launch used the work queue
+    int sched_mode = -1, sched_waves = 0;  // torj_set_sched
+    void *d_fit = nullptr;                 // reference-faithful deposition workspace
+    size_t fit_cap = 0;
     double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
     size_t ws_cap = 0;
     int n_cu = 256;
@@ -778,6 +887,17 @@ static int ensure_sched(torj_plasma_s *p, size_t bytes) {
     p->sched_cap = 0;
     HIPCK(hipMalloc(&p->d_sched, bytes));
     p->sched_cap = bytes;
+    return 0;
+}
+
+static int ensure_fit(torj_plasma_s *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->fit_cap >= bytes) return 0;
+    if (p->d_fit) HIPCK(hipFree(p->d_fit));
+    p->d_fit = nullptr;
+    p->fit_cap = 0;
+    HIPCK(hipMalloc(&p->d_fit, bytes));
+    p->fit_cap = bytes;
     return 0;
 }
 
@@ -994,6 +1114,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->d_coef) (void)hipFree(p->d_coef);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
+    if (p->d_fit) (void)hipFree(p->d_fit);
     if (p->d_ws) (void)hipFree(p->d_ws);
     delete p;
     return 0;
@@ -1302,13 +1423,26 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
                       const double *N0, const double *weights, int n_psi, const double *grid,
                       double *state, int *status, int *steps, double *dP, double *Pdep,
                       double *traj, uint64_t *counters, void *stream) {
+    return torj_trace_device_ex(p, cfg, n, x0, N0, weights, n_psi, grid, nullptr, nullptr, state,
+                                status, steps, dP, Pdep, traj, counters, stream);
+}
+
+int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                         const double *N0, const double *weights, int n_psi, const double *grid,
+                         const double *x_launch, const double *s0, double *state, int *status,
+                         int *steps, double *dP, double *Pdep, double *traj, uint64_t *counters,
+                         void *stream) {
     if (!p || !cfg) return fail("bad plasma handle or cfg");
     if (n <= 0) return 0;
     if (!x0 || !N0 || !state || !status || !steps) return fail("x0, N0, state, status, steps required");
     if (cfg->n_steps < 0) return fail("n_steps < 0");
     if (cfg->mode != 1 && cfg->mode != -1) return fail("mode must be +1 (X) or -1 (O)");
     if (!(cfg->ds > 0)) return fail("ds must be > 0");
+    if (cfg->deposition != 0 && cfg->deposition != 1) return fail("deposition must be 0 or 1");
     const bool depo = n_psi >= 2 && grid && dP;
+    const bool fit = depo && cfg->deposition == 1;
+    if (fit && (!x_launch || !s0))
+        return fail("deposition = 1 (reference profile) needs x_launch and s0 (torj_trace_ex)");
     const bool tr = cfg->traj_stride > 0 && traj;
     if (ensure_device(p)) return -1;
     if (cfg->absorption && ensure_gl_on_device(p->device)) return -1;
@@ -1342,6 +1476,58 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
         }
         a.Pdep = Pdep;
     }
+    FitArgs fa{};
+    if (fit) {
+        // samples (psi, dP/ds) per step, Thomas/second-derivative arrays,
+        // per-boundary root counts, per-shell open-root integrals
+        const size_t K = (size_t)cfg->n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
+        const size_t b_smp = 2 * K * N * sizeof(double), b_m = 3 * K * N * sizeof(double);
+        const size_t b_cnt = (L * N + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
+        const size_t b_ks = (N * sizeof(int) + 255) & ~(size_t)255;
+        if (ensure_fit(p, b_smp + b_m + b_cnt + 2 * b_fo + b_ks)) return -1;
+        char *base = (char *)p->d_fit;
+        a.smp_psi = (double *)base;
+        a.smp_dpds = a.smp_psi + K * N;
+        fa.cp = (double *)(base + b_smp);
+        fa.Mpsi = fa.cp + K * N;
+        fa.MP = fa.Mpsi + K * N;
+        fa.cnt = (unsigned char *)(base + b_smp + b_m);
+        fa.Fopen = (double *)(base + b_smp + b_m + b_cnt);
+        fa.dPs = fa.Fopen + L * N;
+        fa.kstar = (int *)(base + b_smp + b_m + b_cnt + 2 * b_fo);
+        HIPCK(hipMemsetAsync(fa.cnt, 0, L * N, s));
+        HIPCK(hipMemsetAsync(fa.Fopen, 0xFF, b_fo, s));  // NaN: every shell closed
+        HIPCK(hipMemsetAsync(fa.dPs, 0, b_fo, s));
+        fa.coef = p->d_coef;
+        fa.g = p->g;
+        fa.n = n;
+        fa.n_psi = n_psi;
+        fa.ds = cfg->ds;
+        fa.grid = grid;
+        fa.w = weights;
+        fa.x_launch = x_launch;
+        fa.s0 = s0;
+        fa.steps = steps;
+        fa.smp_psi = a.smp_psi;
+        fa.smp_dpds = a.smp_dpds;
+        fa.dP = dP;
+        fa.Pray = Pdep;
+        // uniform boundaries (np.linspace) get a direct index guess, checked
+        // against the stored values; anything else is binary-searched
+        std::vector<double> hg(n_psi);
+        HIPCK(hipMemcpyAsync(hg.data(), grid, n_psi * sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCK(hipStreamSynchronize(s));
+        const double dg = (hg[n_psi - 1] - hg[0]) / (n_psi - 1);
+        bool uni = dg > 0;
+        for (int k = 0; uni && k < n_psi; k++)
+            uni = std::fabs(hg[k] - (hg[0] + k * dg)) <= 1e-9 * dg;
+        for (int k = 1; k < n_psi; k++)
+            if (!(hg[k] > hg[k - 1])) return fail("psi_dP_dV must be strictly increasing");
+        fa.uniform = uni;
+        fa.g0 = hg[0];
+        fa.ginv = uni ? 1.0 / dg : 0.0;
+    }
+    const int DM = !depo ? kDepoNone : (fit ? kDepoSamples : kDepoBinned);
     if (tr) {
         a.traj_stride = cfg->traj_stride;
         a.n_save = cfg->n_steps / cfg->traj_stride;
@@ -1359,6 +1545,30 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
     // (measured: 42k rays 111 vs 106 ms one-shot; 100k rays 151 vs 174 ms)
     const int use_sched = p->sched_mode >= 0 ? p->sched_mode
                                              : (sched_env && G > p->n_cu * 4 ? 1 : 0);
+// every <absorption, deposition mode, trajectory> instance of a trace kernel
+#define TORJ_DISPATCH_T(L, A, D) \
+    do {                         \
+        if (tr)                  \
+            L(A, D, true);       \
+        else                     \
+            L(A, D, false);      \
+    } while (0)
+#define TORJ_DISPATCH_D(L, A)                                 \
+    do {                                                      \
+        if (DM == kDepoBinned)                                \
+            TORJ_DISPATCH_T(L, A, kDepoBinned);               \
+        else if (DM == kDepoSamples)                          \
+            TORJ_DISPATCH_T(L, A, kDepoSamples);              \
+        else                                                  \
+            TORJ_DISPATCH_T(L, A, kDepoNone);                 \
+    } while (0)
+#define TORJ_DISPATCH_TRACE(L)              \
+    do {                                    \
+        if (cfg->absorption)                \
+            TORJ_DISPATCH_D(L, true);       \
+        else                                \
+            TORJ_DISPATCH_D(L, false);      \
+    } while (0)
     if (use_sched && cfg->n_steps > 0) {
         // W persistent waves: at most 2 per SIMD (4 SIMDs per CU), and fewer
         // than G so the ready queue keeps a backlog (a wave never waits for a
@@ -1380,41 +1590,25 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
         unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
         const dim3 grd(W), blk(64);
 #define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace_sched<A, D, T>), grd, blk, 0, s, a, ctl, slots, S, G, cs)
-        if (cfg->absorption) {
-            if (depo) {
-                if (tr) LAUNCH(true, true, true); else LAUNCH(true, true, false);
-            } else {
-                if (tr) LAUNCH(true, false, true); else LAUNCH(true, false, false);
-            }
-        } else {
-            if (depo) {
-                if (tr) LAUNCH(false, true, true); else LAUNCH(false, true, false);
-            } else {
-                if (tr) LAUNCH(false, false, true); else LAUNCH(false, false, false);
-            }
-        }
+        TORJ_DISPATCH_TRACE(LAUNCH);
 #undef LAUNCH
-        HIPCK(hipGetLastError());
-        return 0;
-    }
-    p->last_sched = false;
-    const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
-#define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
-    if (cfg->absorption) {
-        if (depo) {
-            if (tr) LAUNCH(true, true, true); else LAUNCH(true, true, false);
-        } else {
-            if (tr) LAUNCH(true, false, true); else LAUNCH(true, false, false);
-        }
     } else {
-        if (depo) {
-            if (tr) LAUNCH(false, true, true); else LAUNCH(false, true, false);
-        } else {
-            if (tr) LAUNCH(false, false, true); else LAUNCH(false, false, false);
-        }
-    }
+        p->last_sched = false;
+        const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
+#define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
+        TORJ_DISPATCH_TRACE(LAUNCH);
 #undef LAUNCH
+    }
     HIPCK(hipGetLastError());
+    if (fit) {
+        if (cfg->absorption)
+            hipLaunchKernelGGL(k_final_alpha<true>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_final_alpha<false>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+        hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), 0, s, fa);
+        hipLaunchKernelGGL(k_shell_sum, dim3(n_psi), dim3(256), 0, s, fa);
+        HIPCK(hipGetLastError());
+    }
     return 0;
 }
 
@@ -1430,6 +1624,14 @@ int torj_set_sched(torj_plasma_t p, int mode, int waves) {
 int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                const double *N0, const double *weights, int n_psi, const double *grid,
                double *state, int *status, int *steps, double *dP, double *Pdep, double *traj) {
+    return torj_trace_ex(p, cfg, n, x0, N0, weights, n_psi, grid, nullptr, nullptr, state, status,
+                         steps, dP, Pdep, traj);
+}
+
+int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                  const double *N0, const double *weights, int n_psi, const double *grid,
+                  const double *x_launch, const double *s0, double *state, int *status,
+                  int *steps, double *dP, double *Pdep, double *traj) {
     if (!p || !cfg) return fail("bad plasma handle or cfg");
     if (n <= 0) return 0;
     if (ensure_device(p)) return -1;
@@ -1461,8 +1663,13 @@ int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *
         if (dalloc(&dtraj, (size_t)n_save * 4 * n, true)) return -1;
         B.track(dtraj);
     }
-    if (torj_trace_device(p, cfg, n, dx0, dN0, dw, depo ? n_psi : 0, dgrid, dstate, dstatus, dsteps,
-                          ddP, dPdep, dtraj, nullptr, s))
+    double *dxl = nullptr, *ds0 = nullptr;
+    if (x_launch && s0) {
+        if (dupload(&dxl, x_launch, 3 * (size_t)n, s) || dupload(&ds0, s0, n, s)) return -1;
+        B.track(dxl), B.track(ds0);
+    }
+    if (torj_trace_device_ex(p, cfg, n, dx0, dN0, dw, depo ? n_psi : 0, dgrid, dxl, ds0, dstate,
+                             dstatus, dsteps, ddP, dPdep, dtraj, nullptr, s))
         return -1;
     if (ddownload(state, dstate, 7 * (size_t)n, s) || ddownload(status, dstatus, n, s) ||
         ddownload(steps, dsteps, n, s))

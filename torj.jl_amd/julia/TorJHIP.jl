@@ -24,6 +24,7 @@ struct TraceCfg              # torj_trace_cfg
     P_min::Float64
     absorption::Cint
     traj_stride::Cint
+    deposition::Cint         # 0: binned, 1: power_deposition_profile (src/plasma.jl:91-151)
 end
 
 check(rc) = rc == 0 || error(unsafe_string(ccall((:torj_last_error, libtorj), Cstring, ())))
@@ -52,11 +53,11 @@ mutable struct GPUPlasma
     end
 end
 
-"""first_point + vacuum_plasma_refraction for n rays (x0, N0: n x 3)."""
+"""first_point + vacuum_plasma_refraction for n rays (x0, N0: n x 3), on the GPU."""
 function ray_entry(p::GPUPlasma, x0::Matrix{Float64}, N0::Matrix{Float64}, omega, mode)
     n = size(x0, 1)
     xp, Np, s0, st = zeros(n, 3), zeros(n, 3), zeros(n), zeros(Cint, n)
-    check(ccall((:torj_ray_entry, libtorj), Cint,
+    check(ccall((:torj_ray_entry_gpu, libtorj), Cint,
                 (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}, Float64, Cint, Ptr{Float64},
                  Ptr{Float64}, Ptr{Float64}, Ptr{Cint}),
                 p.h, n, x0, N0, omega, mode, xp, Np, s0, st))
@@ -64,18 +65,19 @@ function ray_entry(p::GPUPlasma, x0::Matrix{Float64}, N0::Matrix{Float64}, omega
 end
 
 function trace(p::GPUPlasma, cfg::TraceCfg, x0::Matrix{Float64}, N0::Matrix{Float64},
-               w::Vector{Float64}, psi_grid::Vector{Float64})
+               w::Vector{Float64}, psi_grid::Vector{Float64}, x_launch::Matrix{Float64},
+               s0::Vector{Float64})
     n = size(x0, 1)
     n_save = cfg.traj_stride > 0 ? cfg.n_steps ÷ cfg.traj_stride : 0
     state, status, steps = zeros(n, 7), zeros(Cint, n), zeros(Cint, n)
     dP, Pdep, traj = zeros(length(psi_grid) + 1), zeros(n), zeros(n, 4, max(n_save, 1))
-    GC.@preserve x0 N0 w psi_grid begin
-        check(ccall((:torj_trace, libtorj), Cint,
+    GC.@preserve x0 N0 w psi_grid x_launch s0 begin
+        check(ccall((:torj_trace_ex, libtorj), Cint,
                     (Ptr{Cvoid}, Ref{TraceCfg}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
-                     Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Cint}, Ptr{Cint}, Ptr{Float64},
-                     Ptr{Float64}, Ptr{Float64}),
-                    p.h, cfg, n, x0, N0, w, length(psi_grid), psi_grid, state, status, steps, dP,
-                    Pdep, n_save > 0 ? traj : C_NULL))
+                     Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Cint},
+                     Ptr{Cint}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                    p.h, cfg, n, x0, N0, w, length(psi_grid), psi_grid, x_launch, s0, state,
+                    status, steps, dP, Pdep, n_save > 0 ? traj : C_NULL))
     end
     return state, status, steps, dP, Pdep, traj
 end
@@ -89,15 +91,17 @@ end
 
 """make_ray -- same signature and return tuple as TorJ.make_ray (src/solve.jl:135-181)."""
 function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f::Real,
-                  mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4)
+                  mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4,
+                  deposition::Integer=1)
     ω = 2π * f
     xp, Np, s0, st = ray_entry(p, reshape(collect(Float64, x0), 1, 3),
                                reshape(collect(Float64, N_vacuum), 1, 3), ω, mode)
     st[1] == 0 || throw(AssertionError("ray entry failed (status $(st[1]))"))
     n_steps = max(1, round(Int, s_max / ds))
-    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1)
+    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition)
     g = collect(Float64, psi_dP_dV)
-    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, ones(1), g)
+    xl = reshape(collect(Float64, x0), 1, 3)
+    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, ones(1), g, xl, s0)
     k = steps[1]
     s = vcat(0.0, s0[1], s0[1] .+ ds .* (1:k))
     u = vcat([collect(Float64, x0)], [xp[1, :]], [traj[1, 1:3, i] for i in 1:k])
@@ -112,7 +116,7 @@ uses TorJ.launch_peripheral_rays / IMAS angles on the host, the GPU for every ra
 function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::Integer,
                    s_max::Float64, psi_dP_dV::Vector{Float64}; ds::Float64=1e-4,
                    N_rings::Integer=3, min_azimuthal_points::Integer=5,
-                   normalize_weight_sum::Bool=true)
+                   normalize_weight_sum::Bool=true, deposition::Integer=1)
     N0 = zeros(3)
     ccall((:torj_pol_tor_angles_2_vector, libtorj), Cvoid, (Float64, Float64, Ptr{Float64}),
           pol, tor, N0)
@@ -134,8 +138,8 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     xp, Np, s0, st = ray_entry(p, pos, dirs, ω, mode)
     all(st .== 0) || throw(AssertionError("ray entry failed for $(count(st .!= 0)) rays"))
     n_steps = max(1, round(Int, s_max / ds))
-    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1)
-    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV)
+    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition)
+    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0)
     dP_dV = zeros(length(psi_dP_dV))
     dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, psi_dP_dV)
     arc_lengths = [vcat(0.0, s0[i], s0[i] .+ ds .* (1:steps[i])) for i in 1:n]

@@ -30,7 +30,13 @@ class TraceCfg(C.Structure):
     """torj_trace_cfg"""
     _fields_ = [("omega", C.c_double), ("mode", C.c_int), ("ds", C.c_double),
                 ("n_steps", C.c_int), ("chunk_steps", C.c_int), ("psi_exit", C.c_double),
-                ("P_min", C.c_double), ("absorption", C.c_int), ("traj_stride", C.c_int)]
+                ("P_min", C.c_double), ("absorption", C.c_int), ("traj_stride", C.c_int),
+                ("deposition", C.c_int)]
+
+    def __init__(self, omega, mode, ds, n_steps, chunk_steps, psi_exit, P_min, absorption,
+                 traj_stride, deposition=0):
+        super().__init__(omega, mode, ds, n_steps, chunk_steps, psi_exit, P_min, absorption,
+                         traj_stride, deposition)
 
 
 _SIGS = {
@@ -65,11 +71,15 @@ _SIGS = {
                                      _dp, _dp, _ip]),
     "torj_trace": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                              _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
+    "torj_trace_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
+                                _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p]),
+    "torj_trace_device_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int] +
+                             [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 11),
     "torj_shell_volumes": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp]),
 }
 

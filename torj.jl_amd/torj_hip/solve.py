@@ -54,16 +54,28 @@ class TraceResult:
         return np.exp(-self.state[:, 6])
 
 
+DEPOSITION = {"binned": 0, "reference": 1}
+
+
 def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps: int,
           chunk_steps: int | None = None, psi_exit: float = 1.0, P_min: float = 1e-6,
-          absorption: bool = True, psi_grid=None, weights=None, traj_stride: int = 0) -> TraceResult:
-    """Integrate rays from in-plasma start states (x0, N0: (n, 3)) on the GPU."""
+          absorption: bool = True, psi_grid=None, weights=None, traj_stride: int = 0,
+          deposition: str = "binned", x_launch=None, s0=None) -> TraceResult:
+    """Integrate rays from in-plasma start states (x0, N0: (n, 3)) on the GPU.
+
+    deposition="binned": psi-shell binning of every RK4 step (P_dep = 1 - P_end
+    per ray); "reference": power_deposition_profile's FITPACK semantics
+    (src/plasma.jl:91-151) from make_ray's saved points, which needs the
+    vacuum launch points x_launch (n, 3) and path lengths s0 (n,)."""
     xs, Ns = soa(x0), soa(N0)
     n = xs.shape[1]
     if chunk_steps is None:
         chunk_steps = max(1, n_steps // 100)
+    dmode = DEPOSITION[deposition]
     cfg = TraceCfg(float(omega), int(mode), float(ds), int(n_steps), int(chunk_steps),
-                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride))
+                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride), dmode)
+    xl = soa(x_launch) if x_launch is not None else None
+    sv = f64(s0) if s0 is not None else None
     g = f64(psi_grid) if psi_grid is not None else np.zeros(0)
     n_psi = len(g)
     w = f64(weights) if weights is not None else None
@@ -74,9 +86,9 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
     Pdep = np.zeros(n)
     n_save = n_steps // traj_stride if traj_stride > 0 else 0
     traj = np.zeros((n_save, 4, n)) if n_save > 0 else None
-    check(lib().torj_trace(plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi,
-                           dptr(g) if n_psi else None, dptr(state), iptr(status), iptr(steps),
-                           dptr(dP), dptr(Pdep), dptr(traj)))
+    check(lib().torj_trace_ex(plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi,
+                              dptr(g) if n_psi else None, dptr(xl), dptr(sv), dptr(state),
+                              iptr(status), iptr(steps), dptr(dP), dptr(Pdep), dptr(traj)))
     return TraceResult(state.T.copy(), status, steps, dP, Pdep,
                        traj.transpose(2, 0, 1).copy() if traj is not None else None)
 
@@ -86,8 +98,10 @@ def _steps_for(s_max: float, ds: float) -> int:
 
 
 def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV, *,
-             ds: float = 1e-4):
-    """make_ray (src/solve.jl:135-181) -> (s, u, P_beam, dP_dV_ray, deposited_power)."""
+             ds: float = 1e-4, deposition: str = "reference"):
+    """make_ray (src/solve.jl:135-181) -> (s, u, P_beam, dP_dV_ray, deposited_power).
+    deposition="reference" (default) follows power_deposition_profile; "binned"
+    uses the in-kernel shell binning."""
     omega = 2.0 * np.pi * f
     x0 = f64(x0)
     xp, Np, s0, st = ray_entry(plasma, x0[None], f64(N_vacuum)[None], omega, mode)
@@ -95,7 +109,8 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
         raise RayEntryError(f"ray entry failed: {STATUS_NAMES[st[0]]}")
     n_steps = _steps_for(s_max, ds)
     g = f64(psi_dP_dV)
-    r = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, traj_stride=1)
+    r = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, traj_stride=1,
+              deposition=deposition, x_launch=x0[None], s0=s0)
     k = int(r.steps[0])
     s = np.concatenate([[0.0, s0[0]], s0[0] + ds * np.arange(1, k + 1)])
     u = np.vstack([x0[None], xp, r.traj[0, :k, :3]])
@@ -109,7 +124,7 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
 def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
               steering_angle_pol: float, spot_size: float, inverse_curvature_radius: float,
               f: float, mode: int, s_max: float, psi_dP_dV, *, ds: float = 1e-4,
-              traj_stride: int = 1, **kwargs):
+              traj_stride: int = 1, deposition: str = "reference", **kwargs):
     """make_beam (src/solve.jl:209-242) -> (arc_lengths, trajectories, ray_powers, dP_dV,
     deposited_power, ray_weights).  kwargs go to launch_peripheral_rays."""
     omega = 2.0 * np.pi * f
@@ -124,7 +139,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     n_steps = _steps_for(s_max, ds)
     g = f64(psi_dP_dV)
     res = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, weights=w,
-                traj_stride=traj_stride)
+                traj_stride=traj_stride, deposition=deposition, x_launch=pos, s0=s0)
     dV = plasma.shell_volumes(g)
     dP_dV = np.zeros(len(g))
     dP_dV[:-1] = res.dP_shell[:len(g) - 1] / dV
