@@ -148,6 +148,7 @@ def main():
     torch.cuda.synchronize(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
+    T._lib.check(L.torj_timing(plasma.handle, 1))  # library HIP events around each phase
     t0 = time.perf_counter()
     for k in range(args.steps):
         one_step(evs[k])
@@ -156,10 +157,17 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    hot_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # whole torj_trace_device_ex call
+    import ctypes
+    n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+    T._lib.check(L.torj_timing_read(plasma.handle, ctypes.byref(n_calls), ctypes.byref(t_trace),
+                                    ctypes.byref(t_post)))
+    T._lib.check(L.torj_timing(plasma.handle, 0))
+    kern_ms = t_trace.value / max(n_calls.value, 1)  # the trace kernel alone
+    post_ms = t_post.value / max(n_calls.value, 1)   # deposition kernels (reference mode)
     tot_steps = torch.tensor([ray_steps_local], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    km = torch.tensor([kern_ms], dtype=torch.float64, device=dev)
+    km = torch.tensor([kern_ms, post_ms, hot_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(tot_steps)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
@@ -174,9 +182,10 @@ def main():
         flop = F.algorithmic_flops(cnt, n_gl=24)
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         sched = os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd
-        kname = "k_trace_sched<1,1,1>" if sched else "k_trace<1,1,1>"
+        dm = 2 if args.deposition == "reference" else 1
+        kname = f"k_trace_sched<1,{dm},1>" if sched else f"k_trace<1,{dm},1>"
         traffic = measured_traffic(kname, n, args)
-        kern_s = float(km.item()) / 1e3
+        kern_s = float(km[0].item()) / 1e3
         achieved = flop / kern_s / 1e12
         out = {
             "metric": "ray-steps/sec, 1e5-ray EC fan on 1 MI355X (+ 2/4/8-GPU scaling)",
@@ -215,6 +224,8 @@ def main():
                 "traffic_source": traffic["file"] if traffic else None,
                 "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
+                "deposition_kernels_ms": float(km[1].item()),
+                "hot_path_ms": float(km[2].item()),
                 "algorithmic_flop_per_launch": flop,
                 "flop_per_ray_step": flop / max(cnt[0], 1),
             },
@@ -276,7 +287,8 @@ def measured_traffic(kname, n, args):
     profiles/<round>/traffic.json; used only if it was taken on this workload
     and kernel (PMC collection cannot run inside the timed process)."""
     import glob
-    base = kname.split("<")[0] + "<"
+    # rocprof's name of the same instance, e.g. "k_trace_sched<true, 2, true>"
+    base = kname.replace("<1,", "<true, ").replace(",1>", ", true>")
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
         try:
             t = json.load(open(f))
@@ -314,7 +326,9 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid):
     steps = int(r["steps"].sum())
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_rays} rays (evenly spaced over the same fan) x {args.n_steps} RK4 steps, "
-                      f"oracle/torj_oracle.c OpenMP, {steps} ray-steps in {dt:.1f} s"}
+                      f"oracle/torj_oracle.c OpenMP, {steps} ray-steps in {dt:.1f} s (ray stepping "
+                      f"+ binned deposition; the reference profile's FITPACK post-processing is "
+                      f"not included on the CPU side)"}
 
 
 if __name__ == "__main__":

@@ -206,6 +206,15 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
+/* Per-phase HIP-event timing of torj_trace[_device][_ex] calls on this handle
+ * (measurement support, no reference counterpart).  torj_timing(p, 1) clears
+ * and enables recording: events on the call's stream before the trace kernel,
+ * after it, and after the deposition kernels.  torj_timing_read waits for the
+ * recorded calls and returns their count and summed trace-kernel / post-
+ * processing milliseconds, then clears. */
+int torj_timing(torj_plasma_t p, int enable);
+int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post_ms);
+
 /* shell volumes dV[j] = V(psi_grid[j+1]) - V(psi_grid[j]), j < n_psi-1 (host;
  * src/plasma.jl:117-122) */
 int torj_shell_volumes(torj_plasma_t p, int n_psi, const double *psi_grid, double *dV);

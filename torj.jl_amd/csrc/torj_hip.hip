@@ -830,6 +830,9 @@ struct torj_plasma_s {
     int sched_mode = -1, sched_waves = 0;  // torj_set_sched
     void *d_fit = nullptr;                 // reference-faithful deposition workspace
     size_t fit_cap = 0;
+    bool timing = false;                   // torj_timing: HIP events around each phase
+    std::vector<hipEvent_t> ev_pool;       // 3 per recorded call (start, trace end, post end)
+    size_t ev_used = 0;
     double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
     size_t ws_cap = 0;
     int n_cu = 256;
@@ -1115,6 +1118,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
     if (p->d_fit) (void)hipFree(p->d_fit);
+    for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
     delete p;
     return 0;
@@ -1569,6 +1573,19 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         else                                \
             TORJ_DISPATCH_D(L, false);      \
     } while (0)
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (p->timing) {
+        if (p->ev_used + 3 > p->ev_pool.size()) {
+            for (int q = 0; q < 3; q++) {
+                hipEvent_t e;
+                HIPCK(hipEventCreate(&e));
+                p->ev_pool.push_back(e);
+            }
+        }
+        for (int q = 0; q < 3; q++) ev[q] = p->ev_pool[p->ev_used + q];
+        p->ev_used += 3;
+        HIPCK(hipEventRecord(ev[0], s));
+    }
     if (use_sched && cfg->n_steps > 0) {
         // W persistent waves: at most 2 per SIMD (4 SIMDs per CU), and fewer
         // than G so the ready queue keeps a backlog (a wave never waits for a
@@ -1600,6 +1617,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
 #undef LAUNCH
     }
     HIPCK(hipGetLastError());
+    if (ev[1]) HIPCK(hipEventRecord(ev[1], s));
     if (fit) {
         if (cfg->absorption)
             hipLaunchKernelGGL(k_final_alpha<true>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
@@ -1609,6 +1627,32 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         hipLaunchKernelGGL(k_shell_sum, dim3(n_psi), dim3(256), 0, s, fa);
         HIPCK(hipGetLastError());
     }
+    if (ev[2]) HIPCK(hipEventRecord(ev[2], s));
+    return 0;
+}
+
+int torj_timing(torj_plasma_t p, int enable) {
+    if (!p) return fail("bad plasma handle");
+    p->timing = enable != 0;
+    p->ev_used = 0;
+    return 0;
+}
+
+int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post_ms) {
+    if (!p) return fail("bad plasma handle");
+    double t = 0.0, q = 0.0;
+    for (size_t k = 0; k + 3 <= p->ev_used; k += 3) {
+        float a = 0.f, b = 0.f;
+        HIPCK(hipEventSynchronize(p->ev_pool[k + 2]));
+        HIPCK(hipEventElapsedTime(&a, p->ev_pool[k], p->ev_pool[k + 1]));
+        HIPCK(hipEventElapsedTime(&b, p->ev_pool[k + 1], p->ev_pool[k + 2]));
+        t += a;
+        q += b;
+    }
+    if (calls) *calls = (int)(p->ev_used / 3);
+    if (trace_ms) *trace_ms = t;
+    if (post_ms) *post_ms = q;
+    p->ev_used = 0;
     return 0;
 }
 

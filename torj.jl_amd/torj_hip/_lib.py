@@ -74,6 +74,8 @@ _SIGS = {
     "torj_trace_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                                 _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),
+    "torj_timing_read": (C.c_int, [C.c_void_p, _ip, _dp, _dp]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
