@@ -50,6 +50,9 @@ def parse():
     ap.add_argument("--deposition", choices=["binned", "reference"], default="reference",
                     help="binned: in-kernel psi-shell binning; reference: "
                          "power_deposition_profile's FITPACK semantics (extra kernel)")
+    ap.add_argument("--integrator", choices=["rk4", "adaptive"], default="rk4",
+                    help="rk4: fixed steps of ds; adaptive: the reference's solve() semantics "
+                         "(Tsit5, DiffEq step control, dtmax = ds, 100 chunks over n_steps*ds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
@@ -107,12 +110,15 @@ def main():
     d_steps = torch.empty(n, dtype=torch.int32, device=dev)
     d_dP = torch.zeros(args.n_psi + 1, dtype=torch.float64, device=dev)
     d_Pdep = torch.empty(n, dtype=torch.float64, device=dev)
-    n_save = args.n_steps // args.traj_stride if args.traj_stride > 0 else 0
-    d_traj = torch.empty((max(n_save, 1), 4, n), dtype=torch.float64, device=dev)
+    adaptive = args.integrator == "adaptive"
+    cap = 2 * args.n_steps + 400 if adaptive else args.n_steps  # accepted-step capacity
+    n_save = (cap if adaptive else args.n_steps) // args.traj_stride if args.traj_stride > 0 else 0
+    d_traj = torch.empty((max(n_save, 1), 5, n), dtype=torch.float64, device=dev)
     d_cnt = torch.zeros(5, dtype=torch.int64, device=dev)
     dep = 1 if args.deposition == "reference" else 0
-    cfg = T._lib.TraceCfg(omega, args.mode, args.ds, args.n_steps, max(1, args.n_steps // 100),
-                          1.0, 1e-6, 1, args.traj_stride, dep)
+    cfg = T._lib.TraceCfg(omega, args.mode, args.ds, cap, max(1, args.n_steps // 100),
+                          1.0, 1e-6, 1, args.traj_stride, dep, int(adaptive), 1e-6, 1e-6,
+                          args.n_steps * args.ds, 100)
     d_xl, d_s0 = dev_t(pos.T), dev_t(s0)
     L = T.lib()
     stream = torch.cuda.current_stream(dev)
@@ -181,9 +187,10 @@ def main():
         status = d_status.cpu().numpy()
         flop = F.algorithmic_flops(cnt, n_gl=24)
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
-        sched = os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd
+        sched = adaptive or (os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd)
         dm = 2 if args.deposition == "reference" else 1
-        kname = f"k_trace_sched<1,{dm},1>" if sched else f"k_trace<1,{dm},1>"
+        kname = (f"k_trace_sched<true, {dm}, true, {int(adaptive)}>" if sched
+                 else f"k_trace<true, {dm}, true>")  # rocprof's name of the instance
         traffic = measured_traffic(kname, n, args)
         kern_s = float(km[0].item()) / 1e3
         achieved = flop / kern_s / 1e12
@@ -204,7 +211,7 @@ def main():
             "config": {
                 "workload": f"C3: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
                             f"min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, {args.n_steps} RK4 "
-                            f"steps ds={args.ds:g} m, Albajar alpha (GL-24), psi-shell deposition "
+                            f"steps ds={args.ds:g} m ({args.integrator}), Albajar alpha (GL-24), psi-shell deposition "
                             f"n_psi={args.n_psi} ({args.deposition}), traj stride {args.traj_stride}",
                 "rays_per_gpu": n,
                 "rk4_steps": args.n_steps,
@@ -253,7 +260,7 @@ def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps, pos, s0):
     xs, Ns = np.ascontiguousarray(xp.T), np.ascontiguousarray(Np.T)
     state, status, steps = np.zeros((7, n)), np.zeros(n, np.int32), np.zeros(n, np.int32)
     dP, Pdep = np.zeros(len(grid) + 1), np.zeros(n)
-    traj = np.zeros((max(n_save, 1), 4, n))
+    traj = np.zeros((max(n_save, 1), 5, n))
     dp, ip = T._lib.dptr, T._lib.iptr
     t0 = time.perf_counter()
     xl = np.ascontiguousarray(pos.T)
@@ -287,8 +294,7 @@ def measured_traffic(kname, n, args):
     profiles/<round>/traffic.json; used only if it was taken on this workload
     and kernel (PMC collection cannot run inside the timed process)."""
     import glob
-    # rocprof's name of the same instance, e.g. "k_trace_sched<true, 2, true>"
-    base = kname.replace("<1,", "<true, ").replace(",1>", ", true>")
+    base = kname
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
         try:
             t = json.load(open(f))

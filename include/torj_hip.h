@@ -43,7 +43,8 @@ enum torj_status {
     TORJ_RAY_ABSORBED = 2,    /* P < P_min at a chunk boundary (src/solve.jl:176) */
     TORJ_RAY_NAN = 3,         /* non-finite state (e.g. upper-hybrid resonance) */
     TORJ_RAY_REFLECTED = 4,   /* N_s^2 <= 0 at the plasma edge (src/solve.jl:57-59) */
-    TORJ_RAY_ENTRY_FAIL = 5   /* first_point / refraction assertions (src/solve.jl:32,138,141) */
+    TORJ_RAY_ENTRY_FAIL = 5,  /* first_point / refraction assertions (src/solve.jl:32,138,141) */
+    TORJ_RAY_MAX_STEPS = 6    /* integrator 1: accepted-step capacity n_steps exhausted */
 };
 
 typedef struct torj_plasma_s *torj_plasma_t;
@@ -155,6 +156,16 @@ typedef struct {
                             not-a-knot cubic splines of psi(s) and dP/ds = P alpha through
                             make_ray's saved points, boundary roots paired per shell,
                             |integral| per pair, outside-in walk -- needs torj_trace_ex */
+    int integrator;   /* 0: fixed-step classic RK4 of n_steps steps of ds (default);
+                         1: adaptive, as the reference's solve() (src/solve.jl:144-162):
+                            Tsit5 5(4) on u = (x, N, P) with DiffEq's PI step control and
+                            initial-step heuristic, abstol/reltol below, dtmax = ds, over
+                            n_chunks tspans of s_max/n_chunks starting at s0 (each chunk
+                            restarts the integrator); n_steps is then the per-ray capacity
+                            of accepted steps (status MAX_STEPS when exceeded) */
+    double abstol, reltol;  /* integrator 1: 1e-6, 1e-6 in the reference (src/solve.jl:157) */
+    double s_max;     /* integrator 1: path length in the plasma (make_ray's s_max) */
+    int n_chunks;     /* integrator 1: 100 in the reference (src/solve.jl:145) */
 } torj_trace_cfg;
 
 /* Host-pointer form.  x0, N0: in-plasma start states (3 x n); weights (n, may
@@ -163,7 +174,8 @@ typedef struct {
  * status n, steps n; dP_shell n_psi + 1: [j] = sum_rays w * (power deposited
  * in psi shell [psi_grid[j], psi_grid[j+1]]) for j < n_psi-1, [n_psi-1] = 0,
  * [n_psi] = sum_rays w * P_dep(ray); P_dep n (per ray, unweighted).  traj:
- * (n_steps/traj_stride) x 4 x n, NaN after a ray stops.  Any output may be
+ * (n_steps/traj_stride) x 5 x n = (x, y, z, tau, s) every traj_stride (accepted)
+ * steps, s the arc length from the vacuum launch point; NaN after a ray stops.  Any output may be
  * NULL.  Divide dP_shell[j] by the shell volume to get make_beam's dP_dV
  * (src/plasma.jl:141, src/solve.jl:237-240). */
 int torj_trace(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,

@@ -59,7 +59,10 @@ def ray_vectors(x_launch, s0, ds, steps, samples, psi_launch):
     launch point (s = 0, dP/ds = 0), entry point (s0, dP/ds = 0), then every
     RK4 step (src/solve.jl:148-172)."""
     k = int(steps)
-    s = np.concatenate([[0.0, s0], s0 + ds * np.arange(1, k + 1)])
+    if samples.shape[1] > 2:  # the trace's own arc lengths (adaptive steps)
+        s = np.concatenate([[0.0], samples[:k + 1, 2]])
+    else:
+        s = np.concatenate([[0.0, s0], s0 + ds * np.arange(1, k + 1)])
     psi = np.concatenate([[psi_launch], samples[:k + 1, 0]])
     dpds = np.concatenate([[0.0, 0.0], samples[1:k + 1, 1]])
     return s, psi, dpds

@@ -15,7 +15,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libtorj_oracle.so")
 
-OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL = range(6)
+OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL, MAX_STEPS = range(7)
 
 
 def default_threads() -> int:
@@ -177,28 +177,34 @@ class OraclePlasma:
 
     def trace(self, x0, N0, omega, mode, ds, n_steps, chunk_steps=None, psi_exit=1.0,
               P_min=1e-6, absorption=True, psi_grid=None, weights=None, traj_stride=0,
-              n_threads=None, samples=False):
+              n_threads=None, samples=False, integrator=0, abstol=1e-6, reltol=1e-6, s_max=None,
+              n_chunks=100, s0=None):
         """Fixed-step RK4 trace of rays (x0, N0: (n, 3) entry states).  samples=True
-        adds "samples": (n, n_steps+1, 2) = (psi_k, dP/ds_k) at the entry point and
-        every step (make_ray's psi / dP_ds vectors, src/solve.jl:151,171)."""
+        adds "samples": (n, n_steps+1, 3) = (psi_k, dP/ds_k, s_k) at the entry point and
+        every step (make_ray's psi / dP_ds vectors, src/solve.jl:151,171).
+        integrator=1: the reference's adaptive solve() (Tsit5, DiffEq step control,
+        n_chunks tspans over s_max from s0); n_steps is then the step capacity."""
         x0, N0 = _c(x0).reshape(-1, 3), _c(N0).reshape(-1, 3)
         n = x0.shape[0]
         if chunk_steps is None:
             chunk_steps = max(1, n_steps // 100)
         grid = _c(psi_grid) if psi_grid is not None else np.zeros(0)
         n_psi = len(grid)
+        s0a = _c(s0) if s0 is not None else None
         cfg = _TraceCfg(omega, mode, ds, n_steps, chunk_steps, psi_exit, P_min, int(absorption),
-                        n_psi, _p(grid) if n_psi else None, traj_stride)
+                        n_psi, _p(grid) if n_psi else None, traj_stride, int(integrator), abstol,
+                        reltol, float(s_max if s_max is not None else n_steps * ds), n_chunks,
+                        _p(s0a) if s0a is not None else None)
         state = np.zeros((n, 7))
         status = np.zeros(n, dtype=np.int32)
         steps = np.zeros(n, dtype=np.int32)
         dP = np.zeros(max(n_psi, 1))
         Pdep = np.zeros(n)
         n_save = n_steps // traj_stride if traj_stride > 0 else 0
-        traj = np.full((n, max(n_save, 1), 4), np.nan)
+        traj = np.full((n, max(n_save, 1), 5), np.nan)
         w = _c(weights) if weights is not None else None
         nt = n_threads or default_threads()
-        smp = np.zeros((n, n_steps + 1, 2)) if samples else None
+        smp = np.zeros((n, n_steps + 1, 3)) if samples else None
         lib().or_trace_samples(self.ref, C.byref(cfg), n, _p(x0), _p(N0),
                                _p(w) if w is not None else None, _p(state),
                                status.ctypes.data_as(_ip), steps.ctypes.data_as(_ip), _p(dP),
@@ -214,7 +220,9 @@ class _TraceCfg(C.Structure):
     _fields_ = [("omega", C.c_double), ("mode", C.c_int), ("ds", C.c_double),
                 ("n_steps", C.c_int), ("chunk_steps", C.c_int), ("psi_exit", C.c_double),
                 ("P_min", C.c_double), ("absorption", C.c_int), ("n_psi", C.c_int),
-                ("psi_grid", _dp), ("traj_stride", C.c_int)]
+                ("psi_grid", _dp), ("traj_stride", C.c_int), ("integrator", C.c_int),
+                ("abstol", C.c_double), ("reltol", C.c_double), ("s_max", C.c_double),
+                ("n_chunks", C.c_int), ("s0", _dp)]
 
 
 # ---- free functions ----

@@ -18,6 +18,7 @@
 #include "torj_oracle.h"
 
 #include <complex.h>
+#include <float.h>
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
@@ -1170,6 +1171,156 @@ static double deposit(const double *g, int n, double pa, double pb, double dP, d
     return inside;
 }
 
+/* ------------------------------------------------------------------------- */
+/* The reference's integrator: solve(ODEProblem(sys!, u0, tspan; dtmax, abstol, */
+/* reltol), callback) with no algorithm argument (src/solve.jl:154-162; the     */
+/* intended OwrenZen3() lands in the parameter slot).   */
+/* DifferentialEquations then picks its default method, which for a non-stiff  */
+/* problem at reltol = 1e-6 is Tsit5 (OrdinaryDiffEq Tsit5 tableau, PI step     */
+/* controller beta1 = 7/50, beta2 = 2/25, gamma = 9/10, qmin = 1/5, qmax = 10,   */
+/* qold0 = qoldmin = 1e-4, RMS error norm of utilde / (abstol + max(|uprev|,    */
+/* |u|) reltol), Hairer's initial step ode_determine_initdt, tstop snapping     */
+/* within 100 eps).  Parity unpinned: no Julia to run the reference here; this  */
+/* restates OrdinaryDiffEq's published algorithm.  u = (x, N, P), dP/ds = -P a. */
+/* ------------------------------------------------------------------------- */
+static const double TS_A[7][6] = {
+    {0, 0, 0, 0, 0, 0},
+    {0.161, 0, 0, 0, 0, 0},
+    {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
+    {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
+    {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
+    {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401,
+     -0.028269050394068383, 0},
+    {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081,
+     2.324710524099774}};
+static const double TS_BT[7] = {-0.00178001105222577714, -0.0008164344596567469,
+                                0.007880878010261995,    -0.1447110071732629,
+                                0.5823571654525552,      -0.45808210592918697,
+                                0.015151515151515152};
+
+static void rhs7(const or_plasma *p, const double u[7], double omega, int mode, int absorb,
+                 double du[7]) {
+    double a;
+    rhs(p, u, omega, mode, absorb, du, &a);
+    du[6] = -u[6] * a; /* sys!: du[7] = -P alpha (src/solve.jl:113) */
+}
+
+static double rms7(const double v[7]) {
+    double s = 0.0;
+    for (int k = 0; k < 7; k++) s += v[k] * v[k];
+    return sqrt(s / 7.0);
+}
+
+/* ode_determine_initdt (OrdinaryDiffEq initdt.jl), order 5 */
+static double ts_initdt(const or_plasma *p, const or_trace_cfg *c, const double u0[7],
+                        const double f0[7], double dtmax) {
+    double sk[7], t0[7], t1[7], u1[7], f1[7];
+    for (int k = 0; k < 7; k++) {
+        sk[k] = c->abstol + fabs(u0[k]) * c->reltol;
+        t0[k] = u0[k] / sk[k];
+        t1[k] = f0[k] / sk[k];
+    }
+    const double d0 = rms7(t0), d1 = rms7(t1);
+    double dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
+    dt0 = fmin(dt0, dtmax);
+    for (int k = 0; k < 7; k++) u1[k] = u0[k] + dt0 * f0[k];
+    rhs7(p, u1, c->omega, c->mode, c->absorption, f1);
+    int same = 1;
+    for (int k = 0; k < 7; k++) same &= (f0[k] == f1[k]);
+    if (same) return 100.0 * dt0;
+    for (int k = 0; k < 7; k++) t0[k] = (f1[k] - f0[k]) / sk[k];
+    const double d2 = rms7(t0) / dt0;
+    const double m = fmax(d1, d2);
+    const double dt1 = (m <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(m)) / 5.0);
+    return fmin(fmin(100.0 * dt0, dt1), dtmax);
+}
+
+/* one ray of the adaptive integration (u = x, N, P in/out); returns status */
+static int ts_ray(const or_plasma *p, const or_trace_cfg *c, int r, double u[7], double s_start,
+                  double w, double *acc, double *Pdep, int *steps_out, double *traj, int n_save,
+                  double *smp) {
+    const double dtmax = c->ds, s_step = c->s_max / (double)c->n_chunks;
+    const int cap = c->n_steps;
+    int steps = 0, status = OR_OK;
+    double psi_a = or_evaluate(&p->psi, u);
+    double k[7][7], ut[7];
+    for (int ch = 1; ch <= c->n_chunks && status == OR_OK; ch++) {
+        double t = (double)(ch - 1) * s_step + s_start; /* Float64(i-1)*s_step + s0 */
+        const double tf = (double)ch * s_step + s_start;
+        rhs7(p, u, c->omega, c->mode, c->absorption, k[0]); /* fsalfirst */
+        double dt = ts_initdt(p, c, u, k[0], dtmax);
+        double qold = 1e-4, q11 = 0.0;
+        while (t < tf) {
+            if (steps >= cap) { /* no room for another accepted step */
+                status = OR_MAX_STEPS;
+                break;
+            }
+            dt = fmin(fabs(dt), tf - t); /* modify_dt_for_tstops! */
+            for (int s = 1; s < 7; s++) {
+                for (int q = 0; q < 7; q++) {
+                    double a = 0.0;
+                    for (int j = 0; j < s; j++) a += TS_A[s][j] * k[j][q];
+                    ut[q] = u[q] + dt * a;
+                }
+                rhs7(p, ut, c->omega, c->mode, c->absorption, k[s]);
+            }
+            /* ut = u_{n+1} (row 7 = b), k[6] = f(u_{n+1}) (FSAL) */
+            double e[7];
+            int bad = 0;
+            for (int q = 0; q < 7; q++) {
+                double a = 0.0;
+                for (int j = 0; j < 7; j++) a += TS_BT[j] * k[j][q];
+                e[q] = dt * a / (c->abstol + fmax(fabs(u[q]), fabs(ut[q])) * c->reltol);
+                if (!isfinite(ut[q])) bad = 1;
+            }
+            if (bad) {
+                status = OR_NAN;
+                break;
+            }
+            const double EEst = rms7(e);
+            double qq;
+            if (EEst == 0.0) {
+                qq = 1.0 / 10.0;
+            } else {
+                q11 = pow(EEst, 0.14);
+                qq = q11 / pow(qold, 0.08);
+                qq = fmax(1.0 / 10.0, fmin(5.0, qq / 0.9));
+            }
+            if (EEst <= 1.0) { /* accept (qsteady_min = qsteady_max = 1) */
+                qold = fmax(EEst, 1e-4);
+                const double dtnew = dt / qq;
+                double tn = t + dt;
+                if (fabs(tn - tf) < 100.0 * DBL_EPSILON * fmax(fabs(t), fabs(tf))) tn = tf;
+                const double Pa = u[6];
+                memcpy(u, ut, sizeof(double) * 7);
+                memcpy(k[0], k[6], sizeof(double) * 7);
+                t = tn;
+                steps++;
+                const double psi_b = or_evaluate(&p->psi, u);
+                if (smp) {
+                    smp[3 * steps] = psi_b;
+                    smp[3 * steps + 1] = -k[0][6]; /* P alpha at the saved point (FSAL) */
+                    smp[3 * steps + 2] = t;
+                }
+                if (acc && Pdep) *Pdep += deposit(c->psi_grid, c->n_psi, psi_a, psi_b, Pa - u[6], w, acc);
+                psi_a = psi_b;
+                if (n_save > 0 && (steps % c->traj_stride) == 0) {
+                    double *T = traj + ((size_t)r * n_save + steps / c->traj_stride - 1) * 5;
+                    T[0] = u[0], T[1] = u[1], T[2] = u[2], T[3] = -log(u[6]), T[4] = t;
+                }
+                dt = fmin(dtmax, dtnew); /* calc_dt_propose! */
+            } else { /* reject: step_reject_controller!(PIController) */
+                dt /= fmin(5.0, q11 / 0.9);
+            }
+        }
+        if (status != OR_OK) break;
+        if (or_evaluate(&p->psi, u) > c->psi_exit) status = OR_LEFT_PLASMA; /* :174 */
+        else if (u[6] < c->P_min) status = OR_ABSORBED;                      /* :176 */
+    }
+    *steps_out = steps;
+    return status;
+}
+
 int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
              const double *N0, const double *weights, double *out_state, int *out_status,
              int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
@@ -1207,11 +1358,24 @@ int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, co
         int status = OR_OK, steps = 0;
         double psi_a = (n_psi > 0) ? or_evaluate(&p->psi, u) : 0.0;
         double Pdep = 0.0;
-        double *smp = out_samples ? out_samples + (size_t)r * (cfg->n_steps + 1) * 2 : NULL;
+        double *smp = out_samples ? out_samples + (size_t)r * (cfg->n_steps + 1) * 3 : NULL;
+        const double s_start = cfg->s0 ? cfg->s0[r] : 0.0;
         if (smp) {
-            for (int k = 0; k < 2 * (cfg->n_steps + 1); k++) smp[k] = NAN;
+            for (int k = 0; k < 3 * (cfg->n_steps + 1); k++) smp[k] = NAN;
             smp[0] = or_evaluate(&p->psi, u);
             smp[1] = 0.0;
+            smp[2] = s_start;
+        }
+        if (cfg->integrator == 1) {
+            double u7[7] = {u[0], u[1], u[2], u[3], u[4], u[5], 1.0};
+            status = ts_ray(p, cfg, r, u7, s_start, w, acc, n_psi > 0 ? &Pdep : NULL, &steps,
+                            out_traj, n_save, smp);
+            for (int k = 0; k < 6; k++) out_state[7 * r + k] = u7[k];
+            out_state[7 * r + 6] = -log(u7[6]);
+            out_status[r] = status;
+            out_steps[r] = steps;
+            if (out_Pdep) out_Pdep[r] = Pdep;
+            continue;
         }
         for (int s = 0; s < cfg->n_steps; s++) {
             double k1[6], k2[6], k3[6], k4[6], a1, a2, a3, a4, ut[6];
@@ -1240,10 +1404,11 @@ int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, co
             steps = s + 1;
             double psi_b = or_evaluate(&p->psi, u);
             if (smp) { /* dP_ds = P alpha_approx at the saved point (src/solve.jl:171) */
-                smp[2 * steps] = psi_b;
-                smp[2 * steps + 1] =
+                smp[3 * steps] = psi_b;
+                smp[3 * steps + 1] =
                     cfg->absorption ? exp(-tau) * or_alpha_approx(p, u, u + 3, cfg->omega, cfg->mode)
                                     : 0.0;
+                smp[3 * steps + 2] = s_start + steps * ds;
             }
             if (n_psi > 0) {
                 Pdep += deposit(cfg->psi_grid, n_psi, psi_a, psi_b, dP, w, acc);
@@ -1251,11 +1416,12 @@ int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, co
             }
             if (n_save > 0 && (steps % cfg->traj_stride) == 0) {
                 int si = steps / cfg->traj_stride - 1;
-                double *T = out_traj + ((size_t)r * n_save + si) * 4;
+                double *T = out_traj + ((size_t)r * n_save + si) * 5;
                 T[0] = u[0];
                 T[1] = u[1];
                 T[2] = u[2];
                 T[3] = tau;
+                T[4] = s_start + steps * ds;
             }
             if (cfg->chunk_steps > 0 && (steps % cfg->chunk_steps) == 0) {
                 if (psi_b > cfg->psi_exit) { /* src/solve.jl:174 */

@@ -36,6 +36,7 @@ extern "C" {
 #define OR_NAN         3
 #define OR_REFLECTED   4
 #define OR_ENTRY_FAIL  5
+#define OR_MAX_STEPS   6
 
 /* 2-D cubic B-spline with Line() extrapolation (Interpolations.jl
  * cubic_spline_interpolation((r_range,z_range), data; extrapolation_bc=Line()),
@@ -133,21 +134,27 @@ typedef struct {
     int n_psi;               /* 0: no deposition */
     const double *psi_grid;  /* n_psi */
     int traj_stride;         /* 0: no trajectory */
+    /* integrator 1: the reference's adaptive solve() -- see or_trace_samples */
+    int integrator;
+    double abstol, reltol, s_max;
+    int n_chunks;
+    const double *s0;        /* n_rays start arc lengths (tspans begin at s0), may be NULL */
 } or_trace_cfg;
 
 /* x0,N0: n_rays x 3 (ray-major); weights may be NULL (=1).
  * out_state n_rays x 7 (x, N, tau); out_dP n_psi (sum over rays of w*dP per
  * shell, NOT divided by dV); out_Pdep n_rays (unweighted deposited power);
- * out_traj n_rays x n_save x 4 (x,y,z,tau), n_save = n_steps/traj_stride. */
+ * out_traj n_rays x n_save x 5 (x,y,z,tau,s), n_save = n_steps/traj_stride
+ * (integrator 1: n_steps = capacity of accepted steps, s the step's arc length). */
 int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
              const double *N0, const double *weights, double *out_state, int *out_status,
              int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
              int n_threads);
 
 /* Same, plus the per-step samples make_ray stores for power_deposition_profile
- * (src/solve.jl:164-172): out_samples n_rays x (n_steps+1) x 2 =
- * (psi(x_k), dP/ds_k = P_k alpha_approx(x_k, N_k)) for k = 0 (entry point,
- * dP/ds = 0 as the reference's initial vector, :151) .. steps; NaN beyond. */
+ * (src/solve.jl:164-172): out_samples n_rays x (n_steps+1) x 3 =
+ * (psi(x_k), dP/ds_k = P_k alpha_approx(x_k, N_k), s_k) for k = 0 (entry
+ * point, dP/ds = 0 as the reference's initial vector, :151) .. steps; NaN beyond. */
 int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
                      const double *N0, const double *weights, double *out_state, int *out_status,
                      int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,

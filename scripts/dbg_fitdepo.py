@@ -13,7 +13,7 @@ for mode in (1, -1):
     xp, Np, s0, st = T.ray_entry(P, pos, dirs, om, mode)
     grid = np.linspace(0, 1, 250)
     g = T.trace(P, xp, Np, om, mode, n_steps=3000, psi_grid=grid, weights=w, deposition="reference", x_launch=pos, s0=s0)
-    o = OP.trace(xp, Np, om, mode, 1e-4, 3000, psi_grid=grid, weights=w, samples=True)
+    o = OP.trace(xp, Np, om, mode, 1e-4, 3000, psi_grid=grid, weights=w, samples=True, s0=s0)
     dV = np.diff([OP.volume(p) for p in grid]); shell = np.zeros(len(grid) - 1); Pr = np.zeros(len(w))
     for i in range(len(w)):
         sv, psi, dpds = D.ray_vectors(pos[i], s0[i], 1e-4, o["steps"][i], o["samples"][i], OP.evaluate("psi", pos[i]))

@@ -48,7 +48,7 @@ def test_reference_deposition_matches_fitpack(gpu, T, hplasma, oplasma, mode):
     grid = np.linspace(0, 1, 250)
     kw = dict(ds=1e-4, n_steps=3000, psi_grid=grid, weights=w)
     g = T.trace(hplasma, xp, Np, om, mode, deposition="reference", x_launch=pos, s0=s0, **kw)
-    o = oplasma.trace(xp, Np, om, mode, 1e-4, 3000, psi_grid=grid, weights=w, samples=True)
+    o = oplasma.trace(xp, Np, om, mode, 1e-4, 3000, psi_grid=grid, weights=w, samples=True, s0=s0)
     assert np.array_equal(g.steps, o["steps"])
     shell, P = _ref_profile(D, oplasma, pos, s0, 1e-4, o, grid, w)
     scale = np.abs(shell).max()
@@ -84,7 +84,7 @@ def test_reference_deposition_nonuniform_grid_and_exits(gpu, T, hplasma, oplasma
     g = T.trace(hplasma, xp, Np, om, 1, n_steps=6000, chunk_steps=60, psi_grid=grid, weights=w,
                 deposition="reference", x_launch=pos, s0=s0)
     o = oplasma.trace(xp, Np, om, 1, 1e-4, 6000, chunk_steps=60, psi_grid=grid, weights=w,
-                      samples=True)
+                      samples=True, s0=s0)
     assert np.array_equal(g.status, o["status"]) and np.array_equal(g.steps, o["steps"])
     assert T.LEFT_PLASMA in g.status.tolist()
     shell, P = _ref_profile(D, oplasma, pos, s0, 1e-4, o, grid, w)
@@ -108,7 +108,7 @@ def test_make_ray_reference_deposition(gpu, T, hplasma, oplasma):
     sv, u, P_beam, dP_dV, pdep = T.make_ray(hplasma, x0, N0, s["f"], 1, 0.4, grid)
     om = 2 * np.pi * s["f"]
     st, xp, Np, s0 = oplasma.ray_entry(x0, N0, om, 1)
-    o = oplasma.trace(xp[None], Np[None], om, 1, 1e-4, 4000, samples=True)
+    o = oplasma.trace(xp[None], Np[None], om, 1, 1e-4, 4000, samples=True, s0=[s0])
     svr, psi, dpds = D.ray_vectors(x0, s0, 1e-4, o["steps"][0], o["samples"][0],
                                    oplasma.evaluate("psi", x0))
     prof, P = D.power_deposition_profile(svr, psi, dpds, grid, oplasma.volume)

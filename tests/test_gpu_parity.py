@@ -156,7 +156,8 @@ def test_trace_matches_oracle_2000_steps(gpu, T, hplasma, oplasma, fan_states, m
     assert abs(g.dP_shell[-1] - np.sum(w[idx] * o["Pdep"])) <= 1e-10 * max(o["Pdep"].max(), 1e-300)
     assert np.abs(g.P_dep - o["Pdep"]).max() <= 1e-10 * max(o["Pdep"].max(), 1e-300)
     tr = g.traj
-    assert tr.shape == (len(idx), 20, 4)
+    assert tr.shape == (len(idx), 20, 5)
+    assert np.abs(tr[:, :, 4] - o["traj"][:, :, 4]).max() < 1e-12
     assert np.abs(tr[:, :, :3] - o["traj"][:, :, :3]).max() < 1e-10 * 3
     if mode == 1:
         assert np.median(g.P_end) < 0.05  # X2 absorption happens on this path

@@ -43,7 +43,7 @@ struct FitArgs {
     const double *x_launch;  // 3 x n vacuum launch points (s = 0)
     const double *s0;        // n, vacuum path length to the entry point
     const int *steps;        // n
-    const double *smp_psi, *smp_dpds;  // (n_steps + 1) x n
+    const double *smp_psi, *smp_dpds, *smp_s;  // (n_steps + 1) x n (smp_s: arc length s_k)
     double *cp, *Mpsi, *MP;            // (n_steps + 2) x n Thomas / second derivatives
     unsigned char *cnt;                // n_psi x n root counts per boundary
     double *Fopen;                     // (n_psi - 1) x n: F at a shell's open root, NaN = closed
@@ -59,7 +59,7 @@ struct RayData {
     const FitArgs *a;
     int i, m;  // lane's ray, number of points (steps + 2)
     double s0, psiL;
-    __device__ double S(int j) const { return j == 0 ? 0.0 : (j == 1 ? s0 : s0 + (j - 1) * a->ds); }
+    __device__ double S(int j) const { return j == 0 ? 0.0 : a->smp_s[(size_t)(j - 1) * a->n + i]; }
     __device__ double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
     __device__ double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[(size_t)(j - 1) * a->n + i]; }
     __device__ double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[(size_t)(j - 1) * a->n + i]; }

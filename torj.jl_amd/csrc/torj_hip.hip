@@ -131,6 +131,12 @@ struct TraceArgs {
     unsigned long long *counters;
     double *smp_psi;   // DEPO == 2: psi(x_k), (n_steps + 1) x n
     double *smp_dpds;  // DEPO == 2: P_k alpha(x_k), (n_steps + 1) x n
+    double *smp_s;     // DEPO == 2: arc length s_k, (n_steps + 1) x n
+    const double *s0;  // n: arc length at the entry point (null: 0)
+    // integrator 1 (the reference's adaptive solve)
+    double abstol, reltol, s_step;
+    int n_chunks;
+    int *chunk;  // n: chunks done (work-queue visits carry it)
 };
 
 // DEPO modes of the trace kernels
@@ -234,6 +240,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if (r.steps == 0) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
             a.smp_psi[i] = psi_a;
             a.smp_dpds[i] = 0.0;
+            a.smp_s[i] = a.s0 ? a.s0[i] : 0.0;
         }
     }
     const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
@@ -294,7 +301,10 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         double psi_b = 0.0;
         if (DEPO != kDepoNone || check)
             psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
-        if constexpr (DEPO == kDepoSamples) a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
+        if constexpr (DEPO == kDepoSamples) {
+            a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
+            a.smp_s[(size_t)r.steps * a.n + i] = (a.s0 ? a.s0[i] : 0.0) + r.steps * a.ds;
+        }
         if constexpr (DEPO == kDepoBinned) {
             r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
             psi_a = psi_b;
@@ -302,11 +312,12 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if constexpr (TRAJ) {
             if ((r.steps % a.traj_stride) == 0) {
                 const size_t si = (size_t)(r.steps / a.traj_stride - 1);
-                double *T = a.traj + si * 4 * (size_t)a.n + i;
+                double *T = a.traj + si * 5 * (size_t)a.n + i;
                 T[0] = x[0];
                 T[(size_t)a.n] = x[1];
                 T[2 * (size_t)a.n] = x[2];
                 T[3 * (size_t)a.n] = tau;
+                T[4 * (size_t)a.n] = (a.s0 ? a.s0[i] : 0.0) + r.steps * a.ds;
             }
         }
         if (check) {
@@ -351,15 +362,16 @@ __device__ __forceinline__ void store_state(const TraceArgs &a, int i, const Ray
 }
 
 __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long long steps,
-                                               const AlbajarWork &work) {
+                                               unsigned long long rhs, const AlbajarWork &work) {
     if (!a.counters) return;
     const unsigned long long s0 = wave_sum(steps);
+    const unsigned long long s1 = wave_sum(rhs);
     const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
     const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
     const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(a.counters + 0, s0);
-        atomicAdd(a.counters + 1, 4ull * s0);
+        atomicAdd(a.counters + 1, s1);
         atomicAdd(a.counters + 2, s2);
         atomicAdd(a.counters + 3, s3);
         atomicAdd(a.counters + 4, s4);
@@ -381,7 +393,216 @@ __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs 
         if constexpr (DEPO == kDepoBinned) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
         steps = r.steps;
     }
-    flush_counters(a, steps, work);
+    flush_counters(a, steps, 4ull * steps, work);
+}
+
+
+// ---------------------------------------------------------------------------
+// The reference's adaptive integration (integrator 1): one tspan chunk of
+// solve(ODEProblem(sys!, u0, tspan; dtmax, abstol, reltol)) per visit
+// (src/solve.jl:154-177), DifferentialEquations' default non-stiff method
+// Tsit5 with OrdinaryDiffEq's PI controller and initial-step heuristic, on
+// u = (x, N, P) with dP/ds = -P alpha.  The oracle restates the same
+// algorithm (oracle/torj_oracle.c ts_ray); parity with DiffEq is unpinned.
+// The seven stage vectors live in LDS (7 x 7 x 64 lanes x 8 B = 25 KB/wave).
+// ---------------------------------------------------------------------------
+__constant__ double c_ts_a[7][6] = {
+    {0, 0, 0, 0, 0, 0},
+    {0.161, 0, 0, 0, 0, 0},
+    {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
+    {2.897153057105493, -6.359448489975075, 4.3622954328695815, 0, 0, 0},
+    {5.325864828439257, -11.748883564062828, 7.4955393428898365, -0.09249506636175525, 0, 0},
+    {5.86145544294642, -12.92096931784711, 8.159367898576159, -0.071584973281401,
+     -0.028269050394068383, 0},
+    {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081,
+     2.324710524099774}};
+__constant__ double c_ts_bt[7] = {-0.00178001105222577714, -0.0008164344596567469,
+                                  0.007880878010261995,    -0.1447110071732629,
+                                  0.5823571654525552,      -0.45808210592918697,
+                                  0.015151515151515152};
+constexpr int kTsLds = 7 * 7 * 64;  // doubles per wave
+
+template <bool ABS>
+__device__ __forceinline__ void rhs7(const TraceArgs &a, const double u[7], double du[7],
+                                     AlbajarWork &work, unsigned long long &nrhs) {
+    double al;
+    ray_rhs<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, u, u + 3, du, al, &work);
+    du[6] = -u[6] * al;  // sys!: du[7] = -P alpha (src/solve.jl:113)
+    nrhs++;
+}
+
+__device__ __forceinline__ double rms7(const double v[7]) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < 7; q++) s = fma(v[q], v[q], s);
+    return sqrt(s * (1.0 / 7.0));
+}
+
+template <bool ABS, int DEPO, bool TRAJ>
+__device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r, int ch,
+                                double *kl, AlbajarWork &work, unsigned long long &nrhs) {
+    // kl: this wave's LDS stage store, [stage][component][lane].  One RHS call
+    // site: the loop walks the phases fsalfirst (st = -2), the initial-step
+    // probe (st = -1) and the Tsit5 stages 1..6; all lanes stay in lockstep.
+    const int lane = threadIdx.x & 63;
+    auto K = [&](int st, int q) -> double & { return kl[(st * 7 + q) * 64 + lane]; };
+    const double s_start = a.s0 ? a.s0[i] : 0.0;
+    double t = (double)(ch - 1) * a.s_step + s_start;  // Float64(i-1)*s_step + s0
+    const double tf = (double)ch * a.s_step + s_start;
+    double u[7] = {r.x[0], r.x[1], r.x[2], r.N[0], r.N[1], r.N[2], r.tau};  // tau slot holds P
+    double ut[7], dt = 0.0, dt0 = 0.0, d1 = 0.0, qold = 1e-4, q11 = 0.0;
+    double psi_a = 0.0;
+    if constexpr (DEPO == kDepoBinned) psi_a = eval_one(a.coef, a.g, sqrt(u[0] * u[0] + u[1] * u[1]), u[2], F_PSI);
+    DepoAcc dacc = {-1, 0.0};
+    int st = -2;
+#pragma unroll 1
+    for (;;) {
+        if (st == -2) {
+#pragma unroll
+            for (int q = 0; q < 7; q++) ut[q] = u[q];
+        } else if (st == -1) {
+#pragma unroll
+            for (int q = 0; q < 7; q++) ut[q] = fma(dt0, K(0, q), u[q]);
+        } else {
+            if (st == 1 && r.steps >= a.n_steps) {  // no room for another accepted step
+                r.status = ST_MAX_STEPS;
+                break;
+            }
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                double acc = 0.0;
+#pragma unroll 1
+                for (int j = 0; j < st; j++) acc = fma(c_ts_a[st][j], K(j, q), acc);
+                ut[q] = fma(dt, acc, u[q]);
+            }
+        }
+        double kq[7];
+        rhs7<ABS>(a, ut, kq, work, nrhs);
+        if (st == -2) {  // fsalfirst; ode_determine_initdt, first half
+#pragma unroll
+            for (int q = 0; q < 7; q++) K(0, q) = kq[q];
+            double v0[7], v1[7];
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                const double sk = a.abstol + fabs(u[q]) * a.reltol;
+                v0[q] = u[q] / sk;
+                v1[q] = kq[q] / sk;
+            }
+            const double d0 = rms7(v0);
+            d1 = rms7(v1);
+            dt0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : (d0 / d1) / 100.0;
+            dt0 = fmin(dt0, a.ds);
+            st = -1;
+            continue;
+        }
+        if (st == -1) {  // ode_determine_initdt, second half (order 5)
+            bool same = true;
+            double v[7];
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                same &= (K(0, q) == kq[q]);
+                v[q] = (kq[q] - K(0, q)) / (a.abstol + fabs(u[q]) * a.reltol);
+            }
+            if (same) {
+                dt = 100.0 * dt0;
+            } else {
+                const double d2 = rms7(v) / dt0, m = fmax(d1, d2);
+                const double dt1 = (m <= 1e-15) ? fmax(1e-6, dt0 * 1e-3) : pow(10.0, -(2.0 + log10(m)) / 5.0);
+                dt = fmin(fmin(100.0 * dt0, dt1), a.ds);
+            }
+            if (!(t < tf)) break;
+            dt = fmin(fabs(dt), tf - t);  // modify_dt_for_tstops!
+            st = 1;
+            continue;
+        }
+#pragma unroll
+        for (int q = 0; q < 7; q++) K(st, q) = kq[q];
+        if (st < 6) {
+            st++;
+            continue;
+        }
+        // ut = u_{n+1}; stage 6 is f(u_{n+1}) (FSAL): error estimate and step control
+        double e[7];
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < 7; q++) {
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < 7; j++) acc = fma(c_ts_bt[j], K(j, q), acc);
+            e[q] = dt * acc / (a.abstol + fmax(fabs(u[q]), fabs(ut[q])) * a.reltol);
+            bad |= !isfinite(ut[q]);
+        }
+        if (bad) {
+            r.status = ST_NAN;
+            break;
+        }
+        const double EEst = rms7(e);
+        double qq;
+        if (EEst == 0.0) {
+            qq = 0.1;
+        } else {
+            q11 = pow(EEst, 0.14);
+            qq = fmax(0.1, fmin(5.0, (q11 / pow(qold, 0.08)) / 0.9));
+        }
+        if (EEst <= 1.0) {  // accept (qsteady_min = qsteady_max = 1)
+            qold = fmax(EEst, 1e-4);
+            const double dtnew = dt / qq;
+            double tn = t + dt;
+            if (fabs(tn - tf) < 100.0 * 2.220446049250313e-16 * fmax(fabs(t), fabs(tf))) tn = tf;
+            const double Pa = u[6];
+#pragma unroll
+            for (int q = 0; q < 7; q++) {
+                u[q] = ut[q];
+                K(0, q) = K(6, q);
+            }
+            t = tn;
+            r.steps++;
+            if constexpr (DEPO != kDepoNone) {
+                const double psi_b = eval_one(a.coef, a.g, sqrt(u[0] * u[0] + u[1] * u[1]), u[2], F_PSI);
+                if constexpr (DEPO == kDepoSamples) {
+                    const size_t o = (size_t)r.steps * a.n + i;
+                    a.smp_psi[o] = psi_b;
+                    a.smp_dpds[o] = -K(0, 6);  // P alpha at the saved point (FSAL)
+                    a.smp_s[o] = t;
+                }
+                if constexpr (DEPO == kDepoBinned) {
+                    r.Pdep += deposit(a, dacc, psi_a, psi_b, Pa - u[6], w);
+                    psi_a = psi_b;
+                }
+            }
+            if constexpr (TRAJ) {
+                if ((r.steps % a.traj_stride) == 0 && r.steps / a.traj_stride <= a.n_save) {
+                    double *T = a.traj + (size_t)(r.steps / a.traj_stride - 1) * 5 * a.n + i;
+                    T[0] = u[0];
+                    T[(size_t)a.n] = u[1];
+                    T[2 * (size_t)a.n] = u[2];
+                    T[3 * (size_t)a.n] = -log(u[6]);
+                    T[4 * (size_t)a.n] = t;
+                }
+            }
+            dt = fmin(a.ds, dtnew);  // calc_dt_propose! (dtmax)
+            if (!(t < tf)) break;
+        } else {  // reject: step_reject_controller!(PIController)
+            dt /= fmin(5.0, q11 / 0.9);
+        }
+        dt = fmin(fabs(dt), tf - t);  // modify_dt_for_tstops!
+        st = 1;
+    }
+    if constexpr (DEPO == kDepoBinned) {
+        if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        r.x[c] = u[c];
+        r.N[c] = u[3 + c];
+    }
+    r.tau = u[6];
+    if (r.status == ST_OK) {  // chunk-end checks (src/solve.jl:174, :176)
+        if (eval_one(a.coef, a.g, sqrt(u[0] * u[0] + u[1] * u[1]), u[2], F_PSI) > a.psi_exit)
+            r.status = ST_LEFT_PLASMA;
+        else if (u[6] < a.P_min)
+            r.status = ST_ABSORBED;
+    }
 }
 
 // Work-queue kernel (ready-queue of ray groups).
@@ -450,12 +671,13 @@ __device__ __forceinline__ void sched_publish_begin() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool ABS, int DEPO, bool TRAJ>
+template <bool ABS, int DEPO, bool TRAJ, int INTEG>
 __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
                                                                      unsigned long long *slots,
                                                                      unsigned S, int G, int cs) {
+    extern __shared__ double lds_k[];  // integrator 1: Tsit5 stage vectors of this wave
     AlbajarWork work = {0u, 0u, 0u};
-    unsigned long long steps = 0;
+    unsigned long long steps = 0, nrhs = 0;
     for (;;) {
         const unsigned t = sched_pop(ctl, slots, S, (unsigned)G);
         if (t == kGroupExit) break;
@@ -464,8 +686,10 @@ __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a,
         bool alive = false;
         if (i < a.n) {
             RayState r;
+            int ch = 0;
             if (t & 0x80000000u) {
                 load_start(a, i, r);
+                if constexpr (INTEG == 1) r.tau = 1.0;  // the tau slot carries P
             } else {
 #pragma unroll
                 for (int c = 0; c < 3; c++) {
@@ -476,19 +700,45 @@ __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a,
                 r.status = a.status[i];
                 r.steps = a.steps[i];
                 r.Pdep = a.Pdep ? a.Pdep[i] : 0.0;
+                if constexpr (INTEG == 1) ch = a.chunk[i];
             }
-            if (r.status == ST_OK && r.steps < a.n_steps) {
-                const int s0 = r.steps;
-                const int s_end = min(a.n_steps, (s0 / cs + 1) * cs);
-                const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
-                ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, s_end, work);
-                steps += (unsigned long long)(r.steps - s0);
-                alive = r.status == ST_OK && r.steps < a.n_steps;
-                if constexpr (DEPO == kDepoBinned) {
-                    if (!alive) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
+            const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
+            if constexpr (INTEG == 0) {
+                if (r.status == ST_OK && r.steps < a.n_steps) {
+                    const int s0 = r.steps;
+                    const int s_end = min(a.n_steps, (s0 / cs + 1) * cs);
+                    ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, s_end, work);
+                    steps += (unsigned long long)(r.steps - s0);
+                    nrhs += 4ull * (unsigned long long)(r.steps - s0);
+                    alive = r.status == ST_OK && r.steps < a.n_steps;
+                    if constexpr (DEPO == kDepoBinned) {
+                        if (!alive) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
+                    }
                 }
+                store_state(a, i, r);
+            } else {
+                if (r.status == ST_OK && ch < a.n_chunks) {
+                    const int s0 = r.steps;
+                    if constexpr (DEPO == kDepoSamples) {
+                        if (ch == 0) {  // entry point (src/solve.jl:151)
+                            a.smp_psi[i] = eval_one(a.coef, a.g, sqrt(r.x[0] * r.x[0] + r.x[1] * r.x[1]), r.x[2], F_PSI);
+                            a.smp_dpds[i] = 0.0;
+                            a.smp_s[i] = a.s0 ? a.s0[i] : 0.0;
+                        }
+                    }
+                    ch++;
+                    ray_chunk_tsit5<ABS, DEPO, TRAJ>(a, i, w, r, ch, lds_k, work, nrhs);
+                    steps += (unsigned long long)(r.steps - s0);
+                    alive = r.status == ST_OK && ch < a.n_chunks;
+                    if constexpr (DEPO == kDepoBinned) {
+                        if (!alive) atomicAdd(a.dP + a.n_psi, w * r.Pdep);
+                    }
+                }
+                a.chunk[i] = ch;
+                const double P = r.tau;
+                if (!alive) r.tau = -log(P);  // final state carries tau = -ln P
+                store_state(a, i, r);
             }
-            store_state(a, i, r);
         }
         const bool any_alive = __any(alive);
         sched_publish_begin();
@@ -503,7 +753,7 @@ __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a,
             }
         }
     }
-    flush_counters(a, steps, work);
+    flush_counters(a, steps, nrhs, work);
 }
 
 // ---------------------------------------------------------------------------
@@ -828,6 +1078,8 @@ struct torj_plasma_s {
     size_t sched_cap = 0;
     bool last_sched = false;               // last torj_trace_device launch used the work queue
     int sched_mode = -1, sched_waves = 0;  // torj_set_sched
+    int *d_chunk = nullptr;                // integrator 1: chunks done per ray
+    size_t chunk_cap = 0;
     void *d_fit = nullptr;                 // reference-faithful deposition workspace
     size_t fit_cap = 0;
     bool timing = false;                   // torj_timing: HIP events around each phase
@@ -890,6 +1142,17 @@ static int ensure_sched(torj_plasma_s *p, size_t bytes) {
     p->sched_cap = 0;
     HIPCK(hipMalloc(&p->d_sched, bytes));
     p->sched_cap = bytes;
+    return 0;
+}
+
+static int ensure_chunks(torj_plasma_s *p, size_t n) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->chunk_cap >= n) return 0;
+    if (p->d_chunk) HIPCK(hipFree(p->d_chunk));
+    p->d_chunk = nullptr;
+    p->chunk_cap = 0;
+    HIPCK(hipMalloc(&p->d_chunk, n * sizeof(int)));
+    p->chunk_cap = n;
     return 0;
 }
 
@@ -1118,6 +1381,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
     if (p->d_fit) (void)hipFree(p->d_fit);
+    if (p->d_chunk) (void)hipFree(p->d_chunk);
     for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
     delete p;
@@ -1443,6 +1707,10 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     if (cfg->mode != 1 && cfg->mode != -1) return fail("mode must be +1 (X) or -1 (O)");
     if (!(cfg->ds > 0)) return fail("ds must be > 0");
     if (cfg->deposition != 0 && cfg->deposition != 1) return fail("deposition must be 0 or 1");
+    if (cfg->integrator != 0 && cfg->integrator != 1) return fail("integrator must be 0 or 1");
+    if (cfg->integrator == 1 && (!(cfg->s_max > 0) || cfg->n_chunks < 1 || !(cfg->abstol > 0) ||
+                                 !(cfg->reltol > 0) || cfg->n_steps < 1))
+        return fail("integrator 1 needs s_max > 0, n_chunks >= 1, abstol, reltol > 0, n_steps >= 1");
     const bool depo = n_psi >= 2 && grid && dP;
     const bool fit = depo && cfg->deposition == 1;
     if (fit && (!x_launch || !s0))
@@ -1470,6 +1738,15 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     a.status = status;
     a.steps = steps;
     a.counters = (unsigned long long *)counters;
+    a.s0 = s0;
+    if (cfg->integrator == 1) {
+        a.abstol = cfg->abstol;
+        a.reltol = cfg->reltol;
+        a.s_step = cfg->s_max / cfg->n_chunks;
+        a.n_chunks = cfg->n_chunks;
+        if (ensure_chunks(p, (size_t)n)) return -1;
+        a.chunk = p->d_chunk;
+    }
     if (depo) {
         a.n_psi = n_psi;
         a.grid = grid;  // uniform-grid fast path is set up in-kernel from grid[0], grid[n-1]
@@ -1485,13 +1762,14 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         // samples (psi, dP/ds) per step, Thomas/second-derivative arrays,
         // per-boundary root counts, per-shell open-root integrals
         const size_t K = (size_t)cfg->n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
-        const size_t b_smp = 2 * K * N * sizeof(double), b_m = 3 * K * N * sizeof(double);
+        const size_t b_smp = 3 * K * N * sizeof(double), b_m = 3 * K * N * sizeof(double);
         const size_t b_cnt = (L * N + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
         const size_t b_ks = (N * sizeof(int) + 255) & ~(size_t)255;
         if (ensure_fit(p, b_smp + b_m + b_cnt + 2 * b_fo + b_ks)) return -1;
         char *base = (char *)p->d_fit;
         a.smp_psi = (double *)base;
         a.smp_dpds = a.smp_psi + K * N;
+        a.smp_s = a.smp_dpds + K * N;
         fa.cp = (double *)(base + b_smp);
         fa.Mpsi = fa.cp + K * N;
         fa.MP = fa.Mpsi + K * N;
@@ -1514,6 +1792,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         fa.steps = steps;
         fa.smp_psi = a.smp_psi;
         fa.smp_dpds = a.smp_dpds;
+        fa.smp_s = a.smp_s;
         fa.dP = dP;
         fa.Pray = Pdep;
         // uniform boundaries (np.linspace) get a direct index guess, checked
@@ -1537,7 +1816,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         a.n_save = cfg->n_steps / cfg->traj_stride;
         a.traj = traj;
         if (a.n_save > 0)
-            HIPCK(hipMemsetAsync(traj, 0xFF, (size_t)a.n_save * 4 * n * sizeof(double), s));  // NaN
+            HIPCK(hipMemsetAsync(traj, 0xFF, (size_t)a.n_save * 5 * n * sizeof(double), s));  // NaN
     }
     static const int sched_env = [] {
         const char *e = getenv("TORJ_SCHED");
@@ -1547,8 +1826,10 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     const int cs = cfg->chunk_steps > 0 ? cfg->chunk_steps : std::max(cfg->n_steps, 1);
     // default: the queue pays off once the beam exceeds one wave per SIMD
     // (measured: 42k rays 111 vs 106 ms one-shot; 100k rays 151 vs 174 ms)
-    const int use_sched = p->sched_mode >= 0 ? p->sched_mode
-                                             : (sched_env && G > p->n_cu * 4 ? 1 : 0);
+    const bool adaptive = cfg->integrator == 1;
+    const int use_sched = adaptive ? 1  // the adaptive path runs one tspan chunk per visit
+                                   : p->sched_mode >= 0 ? p->sched_mode
+                                                        : (sched_env && G > p->n_cu * 4 ? 1 : 0);
 // every <absorption, deposition mode, trajectory> instance of a trace kernel
 #define TORJ_DISPATCH_T(L, A, D) \
     do {                         \
@@ -1606,7 +1887,14 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         p->last_sched = true;
         unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
         const dim3 grd(W), blk(64);
-#define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace_sched<A, D, T>), grd, blk, 0, s, a, ctl, slots, S, G, cs)
+#define LAUNCH(A, D, T)                                                                            \
+    do {                                                                                           \
+        if (adaptive)                                                                              \
+            hipLaunchKernelGGL((k_trace_sched<A, D, T, 1>), grd, blk, kTsLds * sizeof(double), s, a, \
+                               ctl, slots, S, G, cs);                                              \
+        else                                                                                       \
+            hipLaunchKernelGGL((k_trace_sched<A, D, T, 0>), grd, blk, 0, s, a, ctl, slots, S, G, cs); \
+    } while (0)
         TORJ_DISPATCH_TRACE(LAUNCH);
 #undef LAUNCH
     } else {
@@ -1619,7 +1907,9 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     HIPCK(hipGetLastError());
     if (ev[1]) HIPCK(hipEventRecord(ev[1], s));
     if (fit) {
-        if (cfg->absorption)
+        if (adaptive)
+            ;  // the last accepted step's FSAL stage already gave P alpha there
+        else if (cfg->absorption)
             hipLaunchKernelGGL(k_final_alpha<true>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(k_final_alpha<false>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
@@ -1704,13 +1994,17 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
         return -1;
     B.track(dstate), B.track(dstatus), B.track(dsteps);
     if (traj && n_save > 0) {
-        if (dalloc(&dtraj, (size_t)n_save * 4 * n, true)) return -1;
+        if (dalloc(&dtraj, (size_t)n_save * 5 * n, true)) return -1;
         B.track(dtraj);
     }
     double *dxl = nullptr, *ds0 = nullptr;
-    if (x_launch && s0) {
-        if (dupload(&dxl, x_launch, 3 * (size_t)n, s) || dupload(&ds0, s0, n, s)) return -1;
-        B.track(dxl), B.track(ds0);
+    if (x_launch) {
+        if (dupload(&dxl, x_launch, 3 * (size_t)n, s)) return -1;
+        B.track(dxl);
+    }
+    if (s0) {
+        if (dupload(&ds0, s0, n, s)) return -1;
+        B.track(ds0);
     }
     if (torj_trace_device_ex(p, cfg, n, dx0, dN0, dw, depo ? n_psi : 0, dgrid, dxl, ds0, dstate,
                              dstatus, dsteps, ddP, dPdep, dtraj, nullptr, s))
@@ -1724,7 +2018,7 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
         if (dP) std::fill(dP, dP + (n_psi > 0 ? n_psi + 1 : 1), 0.0);
         if (Pdep) std::fill(Pdep, Pdep + n, 0.0);
     }
-    if (traj && n_save > 0 && ddownload(traj, dtraj, (size_t)n_save * 4 * n, s)) return -1;
+    if (traj && n_save > 0 && ddownload(traj, dtraj, (size_t)n_save * 5 * n, s)) return -1;
     HIPCK(hipStreamSynchronize(s));
     if (p->last_sched) {  // bounded-spin watchdog of the work queue
         SchedCtl ctl;

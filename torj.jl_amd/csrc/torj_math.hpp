@@ -34,7 +34,7 @@ enum Field { F_BR = 0, F_BPHI = 1, F_BZ = 2, F_LNNE = 3, F_LNTE = 4, F_PSI = 5 }
 
 // ray status codes (include/torj_hip.h)
 enum Status { ST_OK = 0, ST_LEFT_PLASMA = 1, ST_ABSORBED = 2, ST_NAN = 3, ST_REFLECTED = 4,
-              ST_ENTRY_FAIL = 5 };
+              ST_ENTRY_FAIL = 5, ST_MAX_STEPS = 6 };
 
 struct Grid {
     int nR, nZ;          // data points (coefficients are (nR+2) x (nZ+2))

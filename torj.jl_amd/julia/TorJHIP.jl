@@ -25,6 +25,11 @@ struct TraceCfg              # torj_trace_cfg
     absorption::Cint
     traj_stride::Cint
     deposition::Cint         # 0: binned, 1: power_deposition_profile (src/plasma.jl:91-151)
+    integrator::Cint         # 0: fixed RK4; 1: the reference's adaptive solve() (Tsit5)
+    abstol::Float64
+    reltol::Float64
+    s_max::Float64
+    n_chunks::Cint
 end
 
 check(rc) = rc == 0 || error(unsafe_string(ccall((:torj_last_error, libtorj), Cstring, ())))
@@ -70,7 +75,7 @@ function trace(p::GPUPlasma, cfg::TraceCfg, x0::Matrix{Float64}, N0::Matrix{Floa
     n = size(x0, 1)
     n_save = cfg.traj_stride > 0 ? cfg.n_steps ÷ cfg.traj_stride : 0
     state, status, steps = zeros(n, 7), zeros(Cint, n), zeros(Cint, n)
-    dP, Pdep, traj = zeros(length(psi_grid) + 1), zeros(n), zeros(n, 4, max(n_save, 1))
+    dP, Pdep, traj = zeros(length(psi_grid) + 1), zeros(n), zeros(n, 5, max(n_save, 1))
     GC.@preserve x0 N0 w psi_grid x_launch s0 begin
         check(ccall((:torj_trace_ex, libtorj), Cint,
                     (Ptr{Cvoid}, Ref{TraceCfg}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
@@ -92,18 +97,20 @@ end
 """make_ray -- same signature and return tuple as TorJ.make_ray (src/solve.jl:135-181)."""
 function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f::Real,
                   mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4,
-                  deposition::Integer=1)
+                  deposition::Integer=1, integrator::Integer=0)
     ω = 2π * f
     xp, Np, s0, st = ray_entry(p, reshape(collect(Float64, x0), 1, 3),
                                reshape(collect(Float64, N_vacuum), 1, 3), ω, mode)
     st[1] == 0 || throw(AssertionError("ray entry failed (status $(st[1]))"))
     n_steps = max(1, round(Int, s_max / ds))
-    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition)
+    cap = integrator == 1 ? 2n_steps + 400 : n_steps
+    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition,
+                   integrator, 1e-6, 1e-6, s_max, 100)
     g = collect(Float64, psi_dP_dV)
     xl = reshape(collect(Float64, x0), 1, 3)
     state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, ones(1), g, xl, s0)
     k = steps[1]
-    s = vcat(0.0, s0[1], s0[1] .+ ds .* (1:k))
+    s = vcat(0.0, s0[1], traj[1, 5, 1:k])
     u = vcat([collect(Float64, x0)], [xp[1, :]], [traj[1, 1:3, i] for i in 1:k])
     P_beam = vcat(1.0, 1.0, exp.(-traj[1, 4, 1:k]))
     dP_dV = zeros(length(g))
@@ -116,7 +123,8 @@ uses TorJ.launch_peripheral_rays / IMAS angles on the host, the GPU for every ra
 function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::Integer,
                    s_max::Float64, psi_dP_dV::Vector{Float64}; ds::Float64=1e-4,
                    N_rings::Integer=3, min_azimuthal_points::Integer=5,
-                   normalize_weight_sum::Bool=true, deposition::Integer=1)
+                   normalize_weight_sum::Bool=true, deposition::Integer=1,
+                   integrator::Integer=0)
     N0 = zeros(3)
     ccall((:torj_pol_tor_angles_2_vector, libtorj), Cvoid, (Float64, Float64, Ptr{Float64}),
           pol, tor, N0)
@@ -138,11 +146,13 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     xp, Np, s0, st = ray_entry(p, pos, dirs, ω, mode)
     all(st .== 0) || throw(AssertionError("ray entry failed for $(count(st .!= 0)) rays"))
     n_steps = max(1, round(Int, s_max / ds))
-    cfg = TraceCfg(ω, mode, ds, n_steps, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition)
+    cap = integrator == 1 ? 2n_steps + 400 : n_steps
+    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition,
+                   integrator, 1e-6, 1e-6, s_max, 100)
     state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0)
     dP_dV = zeros(length(psi_dP_dV))
     dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, psi_dP_dV)
-    arc_lengths = [vcat(0.0, s0[i], s0[i] .+ ds .* (1:steps[i])) for i in 1:n]
+    arc_lengths = [vcat(0.0, s0[i], traj[i, 5, 1:steps[i]]) for i in 1:n]
     trajectories = [vcat([pos[i, :]], [xp[i, :]], [traj[i, 1:3, k] for k in 1:steps[i]]) for i in 1:n]
     ray_powers = [vcat(1.0, 1.0, exp.(-traj[i, 4, 1:steps[i]])) for i in 1:n]
     return arc_lengths, trajectories, ray_powers, dP_dV, dP[end], w

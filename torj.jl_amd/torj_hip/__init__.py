@@ -8,7 +8,7 @@ from .launch import launch_peripheral_rays, pol_tor_angles_2_vector
 from .physics import (abs_Al_init, abs_Albajar_fast, alpha_approx, dispersion_relation,
                       grad_lambda, gradΛ, refractive_index_sq, α_approx)
 from .plasma import B_spline, Plasma, T_e, eval_plasma, evaluate, n_e
-from .solve import (ABSORBED, ENTRY_FAIL, LEFT_PLASMA, NAN, OK, REFLECTED, STATUS_NAMES,
+from .solve import (ABSORBED, ENTRY_FAIL, LEFT_PLASMA, MAX_STEPS, NAN, OK, REFLECTED, STATUS_NAMES,
                     RayEntryError, TraceResult, make_beam, make_ray, ray_entry, trace)
 
 __all__ = [

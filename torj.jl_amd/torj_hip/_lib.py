@@ -31,12 +31,14 @@ class TraceCfg(C.Structure):
     _fields_ = [("omega", C.c_double), ("mode", C.c_int), ("ds", C.c_double),
                 ("n_steps", C.c_int), ("chunk_steps", C.c_int), ("psi_exit", C.c_double),
                 ("P_min", C.c_double), ("absorption", C.c_int), ("traj_stride", C.c_int),
-                ("deposition", C.c_int)]
+                ("deposition", C.c_int), ("integrator", C.c_int), ("abstol", C.c_double),
+                ("reltol", C.c_double), ("s_max", C.c_double), ("n_chunks", C.c_int)]
 
     def __init__(self, omega, mode, ds, n_steps, chunk_steps, psi_exit, P_min, absorption,
-                 traj_stride, deposition=0):
+                 traj_stride, deposition=0, integrator=0, abstol=1e-6, reltol=1e-6, s_max=0.0,
+                 n_chunks=100):
         super().__init__(omega, mode, ds, n_steps, chunk_steps, psi_exit, P_min, absorption,
-                         traj_stride, deposition)
+                         traj_stride, deposition, integrator, abstol, reltol, s_max, n_chunks)
 
 
 _SIGS = {

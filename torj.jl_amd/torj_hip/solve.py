@@ -15,8 +15,8 @@ import numpy as np
 from ._lib import TraceCfg, TorjError, check, dptr, f64, iptr, lib, soa
 from .launch import launch_peripheral_rays, pol_tor_angles_2_vector
 
-OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL = range(6)
-STATUS_NAMES = ("OK", "LEFT_PLASMA", "ABSORBED", "NAN", "REFLECTED", "ENTRY_FAIL")
+OK, LEFT_PLASMA, ABSORBED, NAN, REFLECTED, ENTRY_FAIL, MAX_STEPS = range(7)
+STATUS_NAMES = ("OK", "LEFT_PLASMA", "ABSORBED", "NAN", "REFLECTED", "ENTRY_FAIL", "MAX_STEPS")
 
 
 class RayEntryError(AssertionError):
@@ -47,7 +47,7 @@ class TraceResult:
     steps: np.ndarray     # (n,)
     dP_shell: np.ndarray  # (n_psi + 1,): sum_rays w * dP per shell, [n_psi] = sum w * P_dep
     P_dep: np.ndarray     # (n,)
-    traj: np.ndarray | None  # (n, n_save, 4): x, y, z, tau
+    traj: np.ndarray | None  # (n, n_save, 5): x, y, z, tau, s
 
     @property
     def P_end(self):
@@ -55,25 +55,36 @@ class TraceResult:
 
 
 DEPOSITION = {"binned": 0, "reference": 1}
+INTEGRATOR = {"rk4": 0, "adaptive": 1}
 
 
 def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps: int,
           chunk_steps: int | None = None, psi_exit: float = 1.0, P_min: float = 1e-6,
           absorption: bool = True, psi_grid=None, weights=None, traj_stride: int = 0,
-          deposition: str = "binned", x_launch=None, s0=None) -> TraceResult:
+          deposition: str = "binned", x_launch=None, s0=None, integrator: str = "rk4",
+          abstol: float = 1e-6, reltol: float = 1e-6, s_max: float | None = None,
+          n_chunks: int = 100) -> TraceResult:
     """Integrate rays from in-plasma start states (x0, N0: (n, 3)) on the GPU.
 
-    deposition="binned": psi-shell binning of every RK4 step (P_dep = 1 - P_end
-    per ray); "reference": power_deposition_profile's FITPACK semantics
+    deposition="binned": psi-shell binning of every step (P_dep = 1 - P_end per
+    ray); "reference": power_deposition_profile's FITPACK semantics
     (src/plasma.jl:91-151) from make_ray's saved points, which needs the
-    vacuum launch points x_launch (n, 3) and path lengths s0 (n,)."""
+    vacuum launch points x_launch (n, 3) and path lengths s0 (n,).
+
+    integrator="rk4": n_steps fixed steps of ds; "adaptive": the reference's
+    solve() -- Tsit5 with DiffEq's step control (abstol, reltol, dtmax = ds) over
+    n_chunks tspans covering s_max from s0; n_steps is then the accepted-step
+    capacity per ray (status MAX_STEPS when exceeded)."""
     xs, Ns = soa(x0), soa(N0)
     n = xs.shape[1]
     if chunk_steps is None:
         chunk_steps = max(1, n_steps // 100)
     dmode = DEPOSITION[deposition]
+    imode = INTEGRATOR[integrator]
     cfg = TraceCfg(float(omega), int(mode), float(ds), int(n_steps), int(chunk_steps),
-                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride), dmode)
+                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride), dmode,
+                   imode, float(abstol), float(reltol),
+                   float(s_max if s_max is not None else n_steps * ds), int(n_chunks))
     xl = soa(x_launch) if x_launch is not None else None
     sv = f64(s0) if s0 is not None else None
     g = f64(psi_grid) if psi_grid is not None else np.zeros(0)
@@ -85,7 +96,7 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
     dP = np.zeros(n_psi + 1)
     Pdep = np.zeros(n)
     n_save = n_steps // traj_stride if traj_stride > 0 else 0
-    traj = np.zeros((n_save, 4, n)) if n_save > 0 else None
+    traj = np.zeros((n_save, 5, n)) if n_save > 0 else None
     check(lib().torj_trace_ex(plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi,
                               dptr(g) if n_psi else None, dptr(xl), dptr(sv), dptr(state),
                               iptr(status), iptr(steps), dptr(dP), dptr(Pdep), dptr(traj)))
@@ -98,21 +109,27 @@ def _steps_for(s_max: float, ds: float) -> int:
 
 
 def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV, *,
-             ds: float = 1e-4, deposition: str = "reference"):
+             ds: float = 1e-4, deposition: str = "reference", integrator: str = "rk4",
+             max_steps: int | None = None):
     """make_ray (src/solve.jl:135-181) -> (s, u, P_beam, dP_dV_ray, deposited_power).
     deposition="reference" (default) follows power_deposition_profile; "binned"
-    uses the in-kernel shell binning."""
+    uses the in-kernel shell binning.  integrator="adaptive" runs the reference's
+    solve() semantics (Tsit5, dtmax = ds, 100 chunks); "rk4" fixed steps of ds."""
     omega = 2.0 * np.pi * f
     x0 = f64(x0)
     xp, Np, s0, st = ray_entry(plasma, x0[None], f64(N_vacuum)[None], omega, mode)
     if st[0] != OK:
         raise RayEntryError(f"ray entry failed: {STATUS_NAMES[st[0]]}")
     n_steps = _steps_for(s_max, ds)
+    if integrator == "adaptive":
+        n_steps = max_steps or 2 * n_steps + 400
     g = f64(psi_dP_dV)
     r = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, traj_stride=1,
-              deposition=deposition, x_launch=x0[None], s0=s0)
+              deposition=deposition, x_launch=x0[None], s0=s0, integrator=integrator, s_max=s_max)
+    if r.status[0] == MAX_STEPS:
+        raise RuntimeError("make_ray: accepted-step capacity exhausted (raise max_steps)")
     k = int(r.steps[0])
-    s = np.concatenate([[0.0, s0[0]], s0[0] + ds * np.arange(1, k + 1)])
+    s = np.concatenate([[0.0, s0[0]], r.traj[0, :k, 4]])
     u = np.vstack([x0[None], xp, r.traj[0, :k, :3]])
     P_beam = np.concatenate([[1.0, 1.0], np.exp(-r.traj[0, :k, 3])])
     dV = plasma.shell_volumes(g)
@@ -124,7 +141,8 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
 def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
               steering_angle_pol: float, spot_size: float, inverse_curvature_radius: float,
               f: float, mode: int, s_max: float, psi_dP_dV, *, ds: float = 1e-4,
-              traj_stride: int = 1, deposition: str = "reference", **kwargs):
+              traj_stride: int = 1, deposition: str = "reference", integrator: str = "rk4",
+              max_steps: int | None = None, **kwargs):
     """make_beam (src/solve.jl:209-242) -> (arc_lengths, trajectories, ray_powers, dP_dV,
     deposited_power, ray_weights).  kwargs go to launch_peripheral_rays."""
     omega = 2.0 * np.pi * f
@@ -137,9 +155,14 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
         raise RayEntryError(f"{len(bad)} rays failed entry, first: ray {bad[0]} "
                             f"{STATUS_NAMES[st[bad[0]]]}")
     n_steps = _steps_for(s_max, ds)
+    if integrator == "adaptive":
+        n_steps = max_steps or 2 * n_steps + 400
     g = f64(psi_dP_dV)
     res = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, weights=w,
-                traj_stride=traj_stride, deposition=deposition, x_launch=pos, s0=s0)
+                traj_stride=traj_stride, deposition=deposition, x_launch=pos, s0=s0,
+                integrator=integrator, s_max=s_max)
+    if (res.status == MAX_STEPS).any():
+        raise RuntimeError("make_beam: accepted-step capacity exhausted (raise max_steps)")
     dV = plasma.shell_volumes(g)
     dP_dV = np.zeros(len(g))
     dP_dV[:-1] = res.dP_shell[:len(g) - 1] / dV
@@ -147,7 +170,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     arc_lengths, trajectories, ray_powers = [], [], []
     for i in range(len(w)):
         k = int(res.steps[i]) // traj_stride
-        arc_lengths.append(np.concatenate([[0.0, s0[i]], s0[i] + ds * traj_stride * np.arange(1, k + 1)]))
+        arc_lengths.append(np.concatenate([[0.0, s0[i]], res.traj[i, :k, 4]]))
         trajectories.append(np.vstack([pos[i][None], xp[i][None], res.traj[i, :k, :3]]))
         ray_powers.append(np.concatenate([[1.0, 1.0], np.exp(-res.traj[i, :k, 3])]))
     return arc_lengths, trajectories, ray_powers, dP_dV, deposited_power, w
