@@ -32,6 +32,10 @@ sys.path.insert(0, os.path.join(ROOT, "torj.jl_amd"))
 
 # MI355X fp64 vector peak (spec): 256 CU x 2.4 GHz x 128 flop/clk (64 FMA lanes)
 FP64_VECTOR_PEAK_TFLOPS = 78.6
+ABSORPTION = {"none": 0, "albajar": 1, "warm_wr": 2, "warm_fr": 3}
+ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)",
+              "warm_wr": "warm weakly-relativistic alpha (iwarm=1)",
+              "warm_fr": "warm fully-relativistic alpha (iwarm=3)"}
 
 
 def parse():
@@ -53,6 +57,9 @@ def parse():
     ap.add_argument("--integrator", choices=["rk4", "adaptive"], default="rk4",
                     help="rk4: fixed steps of ds; adaptive: the reference's solve() semantics "
                          "(Tsit5, DiffEq step control, dtmax = ds, 100 chunks over n_steps*ds)")
+    ap.add_argument("--absorption", choices=list(ABSORPTION), default="albajar",
+                    help="albajar: abs_Albajar_fast (C3, the headline); warm_wr / warm_fr: the "
+                         "repaired general_absorption.jl alpha, iwarm 1 (C5) / 3; none: cold")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
@@ -117,7 +124,8 @@ def main():
     d_cnt = torch.zeros(5, dtype=torch.int64, device=dev)
     dep = 1 if args.deposition == "reference" else 0
     cfg = T._lib.TraceCfg(omega, args.mode, args.ds, cap, max(1, args.n_steps // 100),
-                          1.0, 1e-6, 1, args.traj_stride, dep, int(adaptive), 1e-6, 1e-6,
+                          1.0, 1e-6, ABSORPTION[args.absorption], args.traj_stride, dep,
+                          int(adaptive), 1e-6, 1e-6,
                           args.n_steps * args.ds, 100)
     d_xl, d_s0 = dev_t(pos.T), dev_t(s0)
     L = T.lib()
@@ -143,7 +151,7 @@ def main():
     # counted launch (work counters for the algorithmic FLOP figure), also warms up
     d_cnt.zero_()
     launch(d_cnt.data_ptr())
-    torch.cuda.synchronize(dev)
+    T._lib.check(L.torj_trace_check(plasma.handle, stream.cuda_stream))  # all groups retired
     cnt = d_cnt.cpu().numpy().astype(np.int64)
     ray_steps_local = int(cnt[0])
     for _ in range(args.warmup):
@@ -163,6 +171,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
+    T._lib.check(L.torj_trace_check(plasma.handle, stream.cuda_stream))
     hot_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # whole torj_trace_device_ex call
     import ctypes
     n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
@@ -185,15 +194,22 @@ def main():
 
     if rank == 0:
         status = d_status.cpu().numpy()
-        flop = F.algorithmic_flops(cnt, n_gl=24)
+        flop = F.algorithmic_flops(cnt, n_gl=24) if args.absorption in ("albajar", "none") else None
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         sched = adaptive or (os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd)
         dm = 2 if args.deposition == "reference" else 1
-        kname = (f"k_trace_sched<true, {dm}, true, {int(adaptive)}>" if sched
-                 else f"k_trace<true, {dm}, true>")  # rocprof's name of the instance
+        at = min(ABSORPTION[args.absorption], 2)  # ABS template: 0 cold, 1 Albajar, 2 warm
+        kname = (f"k_trace_sched<{at}, {dm}, true, {int(adaptive)}>" if sched
+                 else f"k_trace<{at}, {dm}, true>")  # rocprof's name of the instance
         traffic = measured_traffic(kname, n, args)
         kern_s = float(km[0].item()) / 1e3
-        achieved = flop / kern_s / 1e12
+        flop_source = "algorithmic (torj_hip/flops.py x the kernel's work counters)"
+        if flop is None and traffic and traffic.get("fp64_flops_executed"):
+            # warm alpha: no op-count model; executed fp64 VALU FLOPs of the same
+            # kernel and workload from the committed PMC profile
+            flop = traffic["fp64_flops_executed"]
+            flop_source = f"executed: PMC SQ_INSTS_VALU_*_F64 x 64 lanes ({traffic['file']})"
+        achieved = flop / kern_s / 1e12 if flop is not None else None
         out = {
             "metric": "ray-steps/sec, 1e5-ray EC fan on 1 MI355X (+ 2/4/8-GPU scaling)",
             "value": value,
@@ -209,14 +225,15 @@ def main():
             "data": "synthetic circular-tokamak equilibrium (analytic, sampled on 56x56) + "
                     "launch_peripheral_rays fan",
             "config": {
-                "workload": f"C3: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
+                "workload": f"{'C5' if args.absorption.startswith('warm') else 'C3'}: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
                             f"min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, {args.n_steps} RK4 "
-                            f"steps ds={args.ds:g} m ({args.integrator}), Albajar alpha (GL-24), psi-shell deposition "
+                            f"steps ds={args.ds:g} m ({args.integrator}), {ALPHA_NAME[args.absorption]}, psi-shell deposition "
                             f"n_psi={args.n_psi} ({args.deposition}), traj stride {args.traj_stride}",
                 "rays_per_gpu": n,
                 "rk4_steps": args.n_steps,
                 "n_psi": args.n_psi,
                 "traj_stride": args.traj_stride,
+                "absorption": args.absorption,
                 "parallelism": f"ray-shard x{world} + RCCL all_reduce of dP/dV",
                 "ray_status_counts": {T.STATUS_NAMES[i]: int(c)
                                       for i, c in enumerate(np.bincount(status, minlength=6)) if c},
@@ -226,15 +243,16 @@ def main():
                 "achieved": achieved,
                 "peak": FP64_VECTOR_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": achieved / FP64_VECTOR_PEAK_TFLOPS,
+                "frac": achieved / FP64_VECTOR_PEAK_TFLOPS if achieved is not None else None,
                 "traffic": traffic["traffic_bytes"] if traffic else None,
                 "traffic_source": traffic["file"] if traffic else None,
                 "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
                 "deposition_kernels_ms": float(km[1].item()),
                 "hot_path_ms": float(km[2].item()),
-                "algorithmic_flop_per_launch": flop,
-                "flop_per_ray_step": flop / max(cnt[0], 1),
+                "flop_per_launch": flop,
+                "flop_source": flop_source if flop is not None else None,
+                "flop_per_ray_step": flop / max(cnt[0], 1) if flop is not None else None,
             },
             "work_counters": {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
                               "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
@@ -295,7 +313,7 @@ def measured_traffic(kname, n, args):
     and kernel (PMC collection cannot run inside the timed process)."""
     import glob
     base = kname
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")), reverse=True):
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*traffic.json")), reverse=True):
         try:
             t = json.load(open(f))
         except (OSError, ValueError):
@@ -303,36 +321,53 @@ def measured_traffic(kname, n, args):
         wl = t.get("workload", {})
         if (base in (t.get("kernel") or "") and wl.get("rays") == n
                 and wl.get("rk4_steps") == args.n_steps and wl.get("n_psi") == args.n_psi
-                and wl.get("traj_stride") == args.traj_stride):
+                and wl.get("traj_stride") == args.traj_stride
+                and wl.get("absorption", "albajar") == args.absorption):
             t["file"] = os.path.relpath(f, ROOT)
             return t
     return None
 
 
 def cpu_baseline(eq, xp, Np, w, omega, args, grid):
-    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same rays."""
+    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same rays.
+    Warm models: the C oracle's RK4 with oracle/warm_ref.py's numpy alpha through
+    a callback (serial), on a shorter sample (rays x steps sized to ~cpu_seconds)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from torj_hip import synthetic as S
 
     OP = O.OraclePlasma(*S.plasma_args(eq))
     O.abs_al_init(24)
-    threads = O.default_threads()
-    idx = np.linspace(0, len(w) - 1, num=threads, dtype=int)  # calibration sample
+    model = ABSORPTION[args.absorption]
+    warm = model >= 2
+    threads = 1 if warm else O.default_threads()
+    kw = dict(psi_grid=grid, absorption=model, n_threads=threads)
+    # calibration sample (warm: one ray over its first 50 steps, after a
+    # 2-step call that pays the callback's first-use cost)
+    cal_steps = min(args.n_steps, 50) if warm else args.n_steps
+    idx = np.linspace(0, len(w) - 1, num=threads, dtype=int)
+    if warm:
+        OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, 2, weights=w[idx], **kw)
     t0 = time.perf_counter()
-    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, psi_grid=grid,
-                 weights=w[idx], n_threads=threads)
+    OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, cal_steps, weights=w[idx], **kw)
     t_cal = time.perf_counter() - t0
-    n_rays = int(max(threads, min(len(w), threads * max(1, round(args.cpu_seconds / max(t_cal, 1e-3))))))
+    scale = max(1.0, args.cpu_seconds / max(t_cal, 1e-3))
+    if warm:
+        n_steps = int(min(args.n_steps, cal_steps * scale))
+        n_rays = int(max(1, min(len(w), cal_steps * scale / max(n_steps, 1))))
+    else:
+        n_steps = args.n_steps
+        n_rays = int(max(threads, min(len(w), threads * round(scale))))
     idx = np.linspace(0, len(w) - 1, num=n_rays, dtype=int)
     t0 = time.perf_counter()
-    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, psi_grid=grid,
-                 weights=w[idx], n_threads=threads)
+    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, n_steps, weights=w[idx], **kw)
     dt = time.perf_counter() - t0
     steps = int(r["steps"].sum())
+    what = ("oracle/torj_oracle.c RK4 + oracle/warm_ref.py numpy alpha (callback, serial)" if warm
+            else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n_rays} rays (evenly spaced over the same fan) x {args.n_steps} RK4 steps, "
-                      f"oracle/torj_oracle.c OpenMP, {steps} ray-steps in {dt:.1f} s (ray stepping "
+            "sample": f"{n_rays} rays (evenly spaced over the same fan) x {n_steps} RK4 steps, "
+                      f"{what}, {steps} ray-steps in {dt:.1f} s (ray stepping "
                       f"+ binned deposition; the reference profile's FITPACK post-processing is "
                       f"not included on the CPU side)"}
 

@@ -111,6 +111,15 @@ int torj_abs_albajar_fast(int n, const double *omega, const double *X, const dou
                           const double *N_abs, const double *N_par, const double *Te, int mode,
                           double *alpha);
 /* refractive_index_sq(X, Y, N_par, mode) (src/dispersion.jl:29-32), batched */
+/* Warm-plasma absorption alpha (src/general_absorption.jl:1328-1337, repaired
+ * as described in DESIGN.md): warmdisp's N_perp^2 with the weakly (iwarm 1) or
+ * fully (iwarm 3) relativistic dielectric tensor, lrm = min(5, larmornumber),
+ * alpha = 2 Im(N_perp^2) omega/c / |dD/dN| (inv_dDdN = 1/|dD/dN|); Nperp2 (may
+ * be NULL) receives N_perp^2 as (re, im) pairs.  GPU, batched (host arrays). */
+int torj_alpha_warm(int n, const double *omega, const double *X, const double *Y,
+                    const double *N_abs, const double *N_par, const double *Te,
+                    const double *inv_dDdN, int mode, int iwarm, double *alpha, double *Nperp2);
+
 int torj_refractive_index_sq(int n, const double *X, const double *Y, const double *N_par,
                              int mode, double *out);
 
@@ -149,7 +158,10 @@ typedef struct {
     int chunk_steps;  /* termination checks every chunk_steps (reference: 100 chunks, src/solve.jl:145) */
     double psi_exit;  /* 1.0 in the reference (src/solve.jl:174) */
     double P_min;     /* 1e-6 in the reference (src/solve.jl:176) */
-    int absorption;   /* 1: integrate optical depth with abs_Albajar_fast */
+    int absorption;   /* optical depth model: 0 none; 1 abs_Albajar_fast (src/absorption.jl:191-226);
+                         2 warm weakly relativistic, 3 warm fully relativistic (the repaired
+                         src/general_absorption.jl alpha, :1328-1337; 3 is what it hard-codes,
+                         2 is BASELINE's C5) -- see torj_alpha_warm */
     int traj_stride;  /* 0: no trajectory; else save (x,y,z,tau) every traj_stride steps */
     int deposition;   /* 0: in-kernel psi-shell binning of the RK4 steps (fast, default);
                          1: the reference's power_deposition_profile (src/plasma.jl:91-151):
@@ -217,6 +229,13 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * waves pulling 64-ray groups chunk by chunk from a ready queue.  waves: number
  * of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
+
+/* Waits for `stream` and checks the last trace launched on this handle: for a
+ * work-queue launch, that every ray group retired and the stall watchdog (no
+ * progress anywhere in the grid for 120 s) did not fire.  torj_trace[_ex]
+ * call it themselves; callers of the asynchronous _device calls call it
+ * before trusting the outputs. */
+int torj_trace_check(torj_plasma_t p, void *stream);
 
 /* Per-phase HIP-event timing of torj_trace[_device][_ex] calls on this handle
  * (measurement support, no reference counterpart).  torj_timing(p, 1) clears

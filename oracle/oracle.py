@@ -44,6 +44,7 @@ def lib():
         L.or_abs_albajar_fast.restype = C.c_double
         L.or_abs_albajar_fast.argtypes = [C.c_double] * 6 + [C.c_int]
         L.or_alpha_approx.restype = C.c_double
+        L.or_grad_norm.restype = C.c_double
         L.or_refractive_index_sq.restype = C.c_double
         L.or_refractive_index_sq.argtypes = [C.c_double, C.c_double, C.c_double, C.c_int]
         L.or_dispersion_relation.restype = C.c_double
@@ -56,6 +57,24 @@ def lib():
         L.or_spl2d_eval.argtypes = [C.c_void_p, C.c_double, C.c_double]
         _lib = L
     return _lib
+
+
+_ALPHA_FN = C.CFUNCTYPE(C.c_double, *([C.c_double] * 7), C.c_int, C.c_int)
+_warm_hook = None
+
+
+def _install_warm_hook():
+    """or_set_alpha_hook -> warm_ref.alpha_warm (absorption models 2 / 3)."""
+    global _warm_hook
+    if _warm_hook is None:
+        import warm_ref
+
+        def fn(omega, X, Y, Nabs, Npar, Te, inv, mode, model):
+            return warm_ref.alpha_warm(omega, X, Y, Nabs, Npar, Te, inv, mode,
+                                       1 if model == 2 else 3)[0]
+
+        _warm_hook = _ALPHA_FN(fn)
+        lib().or_set_alpha_hook(_warm_hook)
 
 
 def _p(a):
@@ -164,6 +183,24 @@ class OraclePlasma:
                              _p(du))
         return du
 
+    def grad_norm(self, x, N, omega, mode):
+        """|dD/dN| (src/solve.jl:85-95 normalisation)"""
+        return lib().or_grad_norm(self.ref, _p(_c(x)), _p(_c(N)), C.c_double(omega),
+                                  C.c_int(mode))
+
+    def alpha_model(self, x, N, omega, mode, model):
+        """optical-depth rate of absorption model 0..3 at (x, N), as the trace uses it"""
+        if model == 0:
+            return 0.0
+        if model == 1:
+            return self.alpha_approx(x, N, omega, mode)
+        import warm_ref
+
+        X, Y, Npar, _ = self.eval_plasma(x, N, omega)
+        return warm_ref.alpha_warm(omega, X, Y, float(np.linalg.norm(N)), Npar, self.T_e(x),
+                                   1.0 / self.grad_norm(x, N, omega, mode), mode,
+                                   1 if model == 2 else 3)[0]
+
     def alpha_approx(self, x, N, omega, mode):
         return lib().or_alpha_approx(self.ref, _p(_c(x)), _p(_c(N)), C.c_double(omega),
                                      C.c_int(mode))
@@ -204,6 +241,9 @@ class OraclePlasma:
         traj = np.full((n, max(n_save, 1), 5), np.nan)
         w = _c(weights) if weights is not None else None
         nt = n_threads or default_threads()
+        if int(absorption) >= 2:  # warm alpha from warm_ref via a callback: serial
+            _install_warm_hook()
+            nt = 1
         smp = np.zeros((n, n_steps + 1, 3)) if samples else None
         lib().or_trace_samples(self.ref, C.byref(cfg), n, _p(x0), _p(N0),
                                _p(w) if w is not None else None, _p(state),

@@ -845,6 +845,17 @@ double or_abs_albajar_fast(double omega, double X, double Y, double N_abs, doubl
 }
 
 /* α_approx, src/absorption.jl:228-235 */
+/* |dD/dN| of D = |N|^2 - refractive_index_sq (src/dispersion.jl:34-39): the
+ * normalisation of gradLambda (src/solve.jl:85-95); 1/|dD/dN| is the group-
+ * velocity factor of the warm alpha (general_absorption.jl:1336, repair R4) */
+double or_grad_norm(const or_plasma *p, const double x[3], const double N[3], double omega,
+                    int mode) {
+    dual xc[3] = {dc(x[0]), dc(x[1]), dc(x[2])};
+    dual Nd[3] = {dvar(N[0], 0), dvar(N[1], 1), dvar(N[2], 2)};
+    dual DN = dispersion_d(p, xc, Nd, omega, mode);
+    return sqrt(DN.d[0] * DN.d[0] + DN.d[1] * DN.d[1] + DN.d[2] * DN.d[2]);
+}
+
 double or_alpha_approx(const or_plasma *p, const double x[3], const double N[3],
                        double omega, int mode) {
     double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
@@ -1123,10 +1134,30 @@ int or_ray_entry(const or_plasma *p, const double x0[3], const double N0[3], dou
 /* ------------------------------------------------------------------------- */
 /* trace: fixed-step RK4 of sys! (src/solve.jl:112-114) + deposition          */
 /* ------------------------------------------------------------------------- */
+/* warm absorption (models 2 and 3) is supplied by the caller: the checker is
+ * oracle/warm_ref.py's numpy restatement of src/general_absorption.jl */
+static or_alpha_fn g_alpha_hook = NULL;
+
+void or_set_alpha_hook(or_alpha_fn fn) { g_alpha_hook = fn; }
+
+/* optical-depth rate of model 0 (none), 1 (alpha_approx: abs_Albajar_fast) or
+ * 2 / 3 (warm alpha, iwarm 1 / 3, with v_g_perp = 1/|dD/dN|) */
+static double alpha_model(const or_plasma *p, const double u[6], double omega, int mode,
+                          int model) {
+    if (model == 0) return 0.0;
+    if (model == 1) return or_alpha_approx(p, u, u + 3, omega, mode);
+    if (!g_alpha_hook) return NAN;
+    double X, Y, Npar, b[3];
+    or_eval_plasma(p, u, u + 3, omega, &X, &Y, &Npar, b);
+    const double Nabs = sqrt(u[3] * u[3] + u[4] * u[4] + u[5] * u[5]);
+    return g_alpha_hook(omega, X, Y, Nabs, Npar, or_T_e(p, u),
+                        1.0 / or_grad_norm(p, u, u + 3, omega, mode), mode, model);
+}
+
 static void rhs(const or_plasma *p, const double u[6], double omega, int mode, int absorb,
                 double du[6], double *alpha) {
     or_grad_lambda(p, u, u + 3, omega, mode, du);
-    *alpha = absorb ? or_alpha_approx(p, u, u + 3, omega, mode) : 0.0;
+    *alpha = alpha_model(p, u, omega, mode, absorb);
 }
 
 /* shell index j with grid[j] <= v < grid[j+1]; clamps to [0, n-2] */
@@ -1406,7 +1437,7 @@ int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, co
             if (smp) { /* dP_ds = P alpha_approx at the saved point (src/solve.jl:171) */
                 smp[3 * steps] = psi_b;
                 smp[3 * steps + 1] =
-                    cfg->absorption ? exp(-tau) * or_alpha_approx(p, u, u + 3, cfg->omega, cfg->mode)
+                    cfg->absorption ? exp(-tau) * alpha_model(p, u, cfg->omega, cfg->mode, cfg->absorption)
                                     : 0.0;
                 smp[3 * steps + 2] = s_start + steps * ds;
             }

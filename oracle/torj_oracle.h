@@ -106,6 +106,13 @@ double or_abs_albajar_fast(double omega, double X, double Y, double N_abs, doubl
                            double Te, int mode);
 double or_alpha_approx(const or_plasma *p, const double x[3], const double N[3],
                        double omega, int mode);
+/* |dD/dN| (the gradLambda normalisation, src/solve.jl:85-95) */
+double or_grad_norm(const or_plasma *p, const double x[3], const double N[3], double omega,
+                    int mode);
+/* warm alpha for absorption models 2 / 3 (iwarm 1 / 3): (omega, X, Y, N_abs,
+ * N_par, Te, 1/|dD/dN|, mode, model) -> alpha; supplied by the test harness */
+typedef double (*or_alpha_fn)(double, double, double, double, double, double, double, int, int);
+void or_set_alpha_hook(or_alpha_fn fn);
 
 /* ---- launch, src/launch.jl:24-132 and IMAS.pol_tor_angles_2_vector ---- */
 int or_launch_count(int N_rings, int min_az);
@@ -130,7 +137,7 @@ typedef struct {
     int chunk_steps;
     double psi_exit;
     double P_min;
-    int absorption;
+    int absorption;          /* 0 none, 1 Albajar, 2 / 3 warm (or_set_alpha_hook) */
     int n_psi;               /* 0: no deposition */
     const double *psi_grid;  /* n_psi */
     int traj_stride;         /* 0: no trajectory */

@@ -1,0 +1,36 @@
+// Host build of the product's warm-absorption math (torj.jl_amd/csrc/
+// torj_warm.hpp is __host__ __device__): lets the CPU suite check the special
+// functions and alpha of the device code against scipy / oracle/warm_ref.py
+// without a GPU.  Test harness only; the product calls these on the device.
+#include "torj_warm.hpp"
+
+extern "C" {
+void wh_zetac(int n, const double *x, const double *y, double *out) {
+    for (int i = 0; i < n; i++) {
+        const torj::cplx z = torj::zetac(x[i], y[i]);
+        out[2 * i] = z.re, out[2 * i + 1] = z.im;
+    }
+}
+
+void wh_expei(int n, const double *x, double *out) {
+    for (int i = 0; i < n; i++) out[i] = torj::expei(x[i]);
+}
+
+void wh_ssbi(double z, int n, int l, double *out) {
+    double v[torj::kWarmMaxL + 3];
+    torj::ssbi(z, n, l, v);
+    for (int m = 0; m <= l + 2 - n; m++) out[m] = v[m];
+}
+
+int wh_larmornumber(double yg, double npl, double mu) { return torj::larmornumber(yg, npl, mu); }
+
+void wh_alpha_warm(int n, const double *om, const double *X, const double *Y, const double *Nabs,
+                   const double *Npar, const double *Te, const double *inv, int mode, int iwarm,
+                   double *alpha, double *n2) {
+    for (int i = 0; i < n; i++) {
+        torj::cplx c;
+        alpha[i] = torj::alpha_warm(om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], inv[i], mode, iwarm, &c);
+        n2[2 * i] = c.re, n2[2 * i + 1] = c.im;
+    }
+}
+}

@@ -1,0 +1,125 @@
+"""GPU parity of the warm-plasma absorption models (torj_trace_cfg.absorption
+2 = weakly relativistic, 3 = fully relativistic; the repaired
+src/general_absorption.jl) against oracle/warm_ref.py.
+
+Tolerances (written per test):
+  * point alpha, iwarm 3: N_perp^2 <= 1e-9 relative; alpha <= 1e-8 relative to
+    |alpha| + 1e-9 * 2 |N_perp^2| (omega/c) / |dD/dN| -- the second term is the
+    rounding floor of Im(N_perp^2) when it is tiny against Re(N_perp^2).
+  * point alpha, iwarm 1: Te >= 1 keV, 1e-7 for both.  Below ~1 keV the
+    reference's fsup recursion (:473-561) cancels catastrophically (each level
+    divides by psi^2 or multiplies by phi^2 = mu |alpha_s| ~ 1e3), so two
+    correct restatements (ACM 680 here, scipy wofz in the checker) differ at
+    1e-7..1e-4 there; that is the reference's conditioning, not a defect.
+  * points where warmdisp's fixed-point iteration does not meet its own 1e-4
+    criterion in 100 passes (near the X-mode cutoff / upper-hybrid layer) are
+    excluded: the reference returns an unconverged iterate there.
+  * traces: x, N endpoints <= 1e-10 (they do not depend on alpha); tau <= 1e-9
+    (model 3) / 1e-8 (model 2)."""
+import math
+import warnings
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+C_LIGHT = 2.99792458e8
+
+
+def _sweep(O, n, seed, mode, te_lo):
+    rng = np.random.default_rng(seed)
+    om = np.full(n, 2 * np.pi * 140e9)
+    X = rng.uniform(0.05, 0.9, n)
+    Y = rng.uniform(0.3, 1.4, n)
+    Npar = rng.uniform(-0.5, 0.5, n)
+    Te = 10 ** rng.uniform(math.log10(te_lo), 4.3, n)
+    inv = rng.uniform(0.2, 2.0, n)
+    N2 = np.array([float(O.refractive_index_sq(x, y, p, mode)) for x, y, p in zip(X, Y, Npar)])
+    Nabs = np.sqrt(np.maximum(N2, Npar ** 2 + 1e-3))
+    return om, X, Y, Nabs, Npar, Te, inv
+
+
+@pytest.mark.parametrize("mode", [1, -1])
+@pytest.mark.parametrize("iwarm,te_lo,tol_n2,tol_a", [(3, 10.0, 1e-9, 1e-8), (1, 1e3, 1e-7, 1e-7)])
+def test_alpha_warm_matches_oracle(gpu, O, T, mode, iwarm, te_lo, tol_n2, tol_a):
+    import warm_ref as W
+
+    args = _sweep(O, 256, 7 + iwarm, mode, te_lo)
+    a, n2 = T.alpha_warm(*args, mode=mode, iwarm=iwarm)
+    ar, nr, conv = np.zeros(len(a)), np.zeros(len(a), complex), np.zeros(len(a), bool)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(len(a)):
+            info = {}
+            ar[i], anpr = W.alpha_warm(*[v[i] for v in args], mode, iwarm, info)
+            nr[i], conv[i] = anpr * anpr, info["converged"]
+    assert conv.sum() > 0.8 * len(a)
+    assert np.isfinite(a[conv]).all()
+    both0 = (nr == 0) & (n2 == 0)
+    e_n = np.where(both0, 0.0, np.abs(n2 - nr) / np.maximum(np.abs(nr), 1e-300))
+    om, inv = args[0], args[6]
+    floor = 1e-9 * 2 * np.abs(nr) * om / C_LIGHT * inv
+    e_a = np.abs(a - ar) / (np.abs(ar) + floor + 1e-300)
+    assert e_n[conv].max() <= tol_n2, e_n[conv].max()
+    assert e_a[conv].max() <= tol_a, e_a[conv].max()
+
+
+def test_alpha_warm_cold_limit(gpu, O, T):
+    """mu -> inf (Te = 1 eV): the warm root is the ray's own cold root (R5)."""
+    X, Npar = 0.3, 0.2
+    for mode in (1, -1):
+        for Y in (0.6, 1.3):
+            n2c = float(O.refractive_index_sq(X, Y, Npar, mode))
+            for iwarm in (1, 3):
+                _, n2 = T.alpha_warm(2 * np.pi * 140e9, X, Y, math.sqrt(n2c), Npar, 1.0, 1.0,
+                                     mode=mode, iwarm=iwarm)
+                assert abs(n2.real / (n2c - Npar ** 2) - 1) < 1e-4
+
+
+def _x2_rays(T, hplasma, n_rings=2, min_az=3):
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], s["f_abs_test"],
+                                            N_rings=n_rings, min_azimuthal_points=min_az)
+    om = 2 * np.pi * s["f_abs_test"]
+    xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1)
+    assert (st == 0).all()
+    return pos, xp, Np, s0, w, om
+
+
+@pytest.mark.parametrize("model,tol_tau", [(3, 1e-9), (2, 1e-8)])
+def test_warm_trace_matches_oracle(gpu, T, hplasma, oplasma, model, tol_tau):
+    """X2 fan through the 92.5 GHz resonance: RK4 with the warm alpha at every
+    stage (solve.jl:112-114 with general_absorption's alpha) vs the C oracle's RK4
+    calling warm_ref per stage."""
+    pos, xp, Np, s0, w, om = _x2_rays(T, hplasma)
+    xp, Np = xp[:3], Np[:3]
+    kw = dict(ds=1e-3, n_steps=400, chunk_steps=20)
+    g = T.trace(hplasma, xp, Np, om, 1, absorption=model, traj_stride=20, **kw)
+    o = oplasma.trace(xp, Np, om, 1, 1e-3, 400, chunk_steps=20, absorption=model, traj_stride=20)
+    assert np.array_equal(g.status, o["status"]) and np.array_equal(g.steps, o["steps"])
+    assert np.abs(g.state[:, :6] - o["state"][:, :6]).max() <= 1e-10 * np.abs(o["state"][:, :6]).max()
+    tau_g, tau_o = g.state[:, 6], o["state"][:, 6]
+    assert tau_o.min() > 1.0  # the fan crosses the X2 layer
+    assert np.abs(tau_g - tau_o).max() <= tol_tau * tau_o.max()
+    assert np.abs(g.traj[..., 3] - o["traj"][..., 3]).max() <= tol_tau * tau_o.max()
+    # same rays with the Albajar model: within a few % of the warm optical depth
+    a = T.trace(hplasma, xp, Np, om, 1, absorption=1, **kw)
+    assert np.abs(a.state[:, :6] - g.state[:, :6]).max() <= 1e-10 * np.abs(g.state[:, :6]).max()
+    assert np.abs(a.state[:, 6] / tau_g - 1).max() < 0.03
+
+
+def test_warm_deposition_conserves_power(gpu, T, hplasma):
+    """binned deposition with model 3: sum of shell powers = sum w (1 - P_end)."""
+    pos, xp, Np, s0, w, om = _x2_rays(T, hplasma, n_rings=3, min_az=3)
+    grid = np.linspace(0, 1, 200)
+    r = T.trace(hplasma, xp, Np, om, 1, absorption=3, ds=1e-3, n_steps=600, psi_grid=grid,
+                weights=w)
+    tot = np.dot(w, 1 - np.exp(-r.state[:, 6]))
+    assert tot > 0.5 * w.sum()
+    assert abs(r.dP_shell[:-1].sum() - tot) <= 1e-12 * tot
+    assert abs(r.dP_shell[-1] - tot) <= 1e-12 * tot

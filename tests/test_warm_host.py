@@ -1,0 +1,109 @@
+"""The product's warm-absorption math (torj.jl_amd/csrc/torj_warm.hpp, compiled
+for the host by tests/native/Makefile -- the same source the trace kernels run)
+against scipy and the warm oracle, on CPU.  SURVEY.md section 8(c) KAT (8):
+zetac vs wofz <= 1e-13, expei vs expi; alpha / N_perp^2 vs oracle/warm_ref.py
+with the tolerances of tests/test_gpu_warm.py."""
+import ctypes as C
+import math
+import os
+import subprocess
+import warnings
+
+import numpy as np
+import pytest
+from scipy.special import expi, iv, wofz
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_dp = C.POINTER(C.c_double)
+
+
+@pytest.fixture(scope="module")
+def H():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(HERE, "native")])
+    L = C.CDLL(os.path.join(HERE, "native", "build", "libwarm_host.so"))
+    L.wh_larmornumber.argtypes = [C.c_double, C.c_double, C.c_double]
+    L.wh_ssbi.argtypes = [C.c_double, C.c_int, C.c_int, _dp]
+    return L
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(_dp)
+
+
+@pytest.mark.parametrize("box", [(-3, 3, -3, 3), (-30, 30, -1, 1), (-8, 8, 1e-6, 0.1),
+                                 (-8, 8, -0.1, -1e-6), (-200, 200, 0, 50)])
+def test_zetac_matches_wofz(H, box):
+    """Im z >= 0 is what the tensors use (phim >= 0); for Im z << 0 the reflection
+    2 exp(-z^2) - w(-z) carries a condition number ~ |z|^2 in both libraries."""
+    rng = np.random.default_rng(1)
+    n = 20000
+    x, y = rng.uniform(box[0], box[1], n), rng.uniform(box[2], box[3], n)
+    out = np.zeros(2 * n)
+    H.wh_zetac(n, _d(x), _d(y), _d(out))
+    z = out[0::2] + 1j * out[1::2]
+    ref = 1j * math.sqrt(math.pi) * wofz(x + 1j * y)
+    fin = np.isfinite(ref)
+    assert (np.abs(z - ref)[fin] / np.abs(ref)[fin]).max() <= 1e-13
+
+
+def test_expei_matches_expi(H):
+    rng = np.random.default_rng(2)
+    x = np.concatenate([10 ** rng.uniform(-8, 2.8, 20000), -(10 ** rng.uniform(-8, 2.8, 20000))])
+    out = np.zeros(len(x))
+    H.wh_expei(len(x), _d(x), _d(out))
+    ref = np.exp(-x) * expi(x)
+    assert (np.abs(out - ref) / np.abs(ref)).max() <= 1e-11
+    z = np.zeros(1)
+    H.wh_expei(1, _d(np.zeros(1)), _d(z))
+    assert z[0] == -1.79e308  # -xinf, as the reference (general_absorption.jl:29-60)
+
+
+@pytest.mark.parametrize("z", [1e-3, 0.3, 2.0, 6.0])
+def test_ssbi_matches_bessel(H, z):
+    out = np.zeros(6)
+    H.wh_ssbi(z, 0, 3, out.ctypes.data_as(_dp))
+    ref = [iv(m + 0.5, z) / (z / 2) ** (m + 0.5) for m in range(6)]
+    assert max(abs(a / b - 1) for a, b in zip(out, ref)) < 1e-9
+
+
+def test_larmornumber_matches_oracle(H):
+    import warm_ref as W
+
+    rng = np.random.default_rng(3)
+    for _ in range(2000):
+        y, npl, mu = rng.uniform(0.2, 1.5), rng.uniform(-0.6, 0.6), 10 ** rng.uniform(1, 4.7)
+        assert H.wh_larmornumber(y, npl, mu) == W.larmornumber(y, npl, mu)
+
+
+@pytest.mark.parametrize("mode", [1, -1])
+@pytest.mark.parametrize("iwarm,te_lo,tol_n2,tol_a", [(3, 10.0, 1e-10, 1e-9), (1, 1e3, 1e-7, 1e-7)])
+def test_alpha_warm_matches_oracle(H, O, mode, iwarm, te_lo, tol_n2, tol_a):
+    import warm_ref as W
+
+    rng = np.random.default_rng(10 + iwarm)
+    n = 200
+    om = np.full(n, 2 * np.pi * 140e9)
+    X, Y = rng.uniform(0.05, 0.9, n), rng.uniform(0.3, 1.4, n)
+    Npar = rng.uniform(-0.5, 0.5, n)
+    Te = 10 ** rng.uniform(math.log10(te_lo), 4.3, n)
+    inv = rng.uniform(0.2, 2.0, n)
+    N2 = np.array([float(O.refractive_index_sq(a, b, c, mode)) for a, b, c in zip(X, Y, Npar)])
+    Nabs = np.sqrt(np.maximum(N2, Npar ** 2 + 1e-3))
+    a, n2 = np.zeros(n), np.zeros(2 * n)
+    H.wh_alpha_warm(n, _d(om), _d(X), _d(Y), _d(Nabs), _d(Npar), _d(Te), _d(inv), mode, iwarm,
+                    a.ctypes.data_as(_dp), n2.ctypes.data_as(_dp))
+    g = n2[0::2] + 1j * n2[1::2]
+    ar, nr, conv = np.zeros(n), np.zeros(n, complex), np.zeros(n, bool)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(n):
+            info = {}
+            ar[i], anpr = W.alpha_warm(om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], inv[i], mode,
+                                       iwarm, info)
+            nr[i], conv[i] = anpr * anpr, info["converged"]
+    both0 = (nr == 0) & (g == 0)
+    e_n = np.where(both0, 0.0, np.abs(g - nr) / np.maximum(np.abs(nr), 1e-300))
+    floor = 1e-9 * 2 * np.abs(nr) * om / 2.99792458e8 * inv
+    e_a = np.abs(a - ar) / (np.abs(ar) + floor + 1e-300)
+    assert conv.sum() > 0.8 * n
+    assert e_n[conv].max() <= tol_n2 and e_a[conv].max() <= tol_a

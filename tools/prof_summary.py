@@ -1,15 +1,18 @@
 #!/usr/bin/env python3
 """Summarise a scripts/profile.sh output directory into profiles/<round>/.
 
-usage: python tools/prof_summary.py gpurun_out/<tag> profiles/r01 [kernel-substring]
-       (the workload is read from the JSON line of <tag>/trace.log)
+usage: python tools/prof_summary.py gpurun_out/<tag> profiles/r01 [kernel-substring] [prefix]
+       (the workload is read from the JSON line of <tag>/trace.log; prefix, e.g.
+       "c5_", names the outputs of a non-headline workload)
 
 Writes
   kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (copied)
   pmc_summary.json   per-dispatch averages of every PMC counter of the hot kernel
   traffic.json       HBM traffic per launch of the hot kernel, from FETCH_SIZE /
                      WRITE_SIZE (KiB) with the gfx950 correction of
-                     MI355X_MICROARCH.md "HBM": FETCH_SIZE x 2
+                     MI355X_MICROARCH.md "HBM": FETCH_SIZE x 2; plus the executed
+                     fp64 FLOPs per launch from the SQ_INSTS_VALU_*_F64 counters
+                     (wave instructions x 64 lanes, FMA x 2: masked lanes count)
 """
 import csv
 import glob
@@ -28,6 +31,7 @@ def workload(src):
                 c = d["config"]
                 return {"rays": c["rays_per_gpu"], "rk4_steps": c["rk4_steps"],
                         "n_psi": c.get("n_psi"), "traj_stride": c.get("traj_stride"),
+                        "absorption": c.get("absorption", "albajar"),
                         "kernel_ms_bench": d["roofline"]["kernel_ms"]}
     except (OSError, ValueError, KeyError):
         pass
@@ -37,11 +41,12 @@ def workload(src):
 def main():
     src, dst = sys.argv[1], sys.argv[2]
     key = sys.argv[3] if len(sys.argv) > 3 else "k_trace"
+    pre = sys.argv[4] if len(sys.argv) > 4 else ""
     os.makedirs(dst, exist_ok=True)
     stats = glob.glob(os.path.join(src, "trace", "*kernel_stats.csv"))
     hot = None
     if stats:
-        shutil.copy(stats[0], os.path.join(dst, "kernel_stats.csv"))
+        shutil.copy(stats[0], os.path.join(dst, pre + "kernel_stats.csv"))
         for r in csv.DictReader(open(stats[0])):
             if key in r["Name"] and (hot is None or float(r["TotalDurationNs"]) > hot[2]):
                 hot = (r["Name"], int(r["Calls"]), float(r["TotalDurationNs"]), float(r["AverageNs"]))
@@ -58,7 +63,7 @@ def main():
     out = {"kernel": meta, "dispatches_per_counter": {k: len(v) for k, v in vals.items()}, "avg": pmc}
     if hot:
         out["kernel_stats"] = {"name": hot[0], "calls": hot[1], "avg_ns": hot[3]}
-    json.dump(out, open(os.path.join(dst, "pmc_summary.json"), "w"), indent=1)
+    json.dump(out, open(os.path.join(dst, pre + "pmc_summary.json"), "w"), indent=1)
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         fetch = 2.0 * pmc["FETCH_SIZE"] * 1024.0  # KiB, half-counted on gfx950
         write = pmc["WRITE_SIZE"] * 1024.0
@@ -67,7 +72,10 @@ def main():
               "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE in separate passes, per-dispatch "
                         "average; FETCH_SIZE x2 (gfx950), KiB -> bytes",
               "source": os.path.basename(os.path.normpath(src)), "workload": workload(src)}
-        json.dump(tr, open(os.path.join(dst, "traffic.json"), "w"), indent=1)
+        f64 = [pmc.get("SQ_INSTS_VALU_" + k + "_F64") for k in ("FMA", "ADD", "MUL", "TRANS")]
+        if all(v is not None for v in f64):
+            tr["fp64_flops_executed"] = 64.0 * (2.0 * f64[0] + f64[1] + f64[2] + f64[3])
+        json.dump(tr, open(os.path.join(dst, pre + "traffic.json"), "w"), indent=1)
         print(json.dumps(tr))
     if hot:
         print(f"{hot[0]}: {hot[1]} calls, avg {hot[3] / 1e6:.2f} ms")

@@ -29,6 +29,7 @@
 #include "torj_math.hpp"
 #include "torj_entry.hpp"
 #include "torj_fitdepo.hpp"
+#include "torj_warm.hpp"
 
 using namespace torj;
 
@@ -132,6 +133,7 @@ struct TraceArgs {
     double *smp_psi;   // DEPO == 2: psi(x_k), (n_steps + 1) x n
     double *smp_dpds;  // DEPO == 2: P_k alpha(x_k), (n_steps + 1) x n
     double *smp_s;     // DEPO == 2: arc length s_k, (n_steps + 1) x n
+    int abs_model;     // 1 Albajar, 2 warm weakly relativistic, 3 warm fully relativistic
     const double *s0;  // n: arc length at the entry point (null: 0)
     // integrator 1 (the reference's adaptive solve)
     double abstol, reltol, s_step;
@@ -226,7 +228,7 @@ struct RayState {
 // src/solve.jl:154-177): classic RK4 of sys!, optical depth, chunk-boundary
 // termination, shell deposition, trajectory samples.  Shared by the one-shot
 // and the work-queue kernels.
-template <bool ABS, int DEPO, bool TRAJ>
+template <int ABS, int DEPO, bool TRAJ>
 __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w, RayState &r,
                                             int s_end, AlbajarWork &work) {
     const GLTable &gl = c_gl;
@@ -255,7 +257,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         }
 #pragma unroll 1
         for (int st = 0; st < 4; st++) {
-            ray_rhs<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, xt, Nt, k, al, &work);
+            ray_rhs_m<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, a.abs_model, xt, Nt, k, al, &work);
             const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
             const double h = (st < 2) ? hds : ds;
 #pragma unroll
@@ -379,7 +381,7 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
 }
 
 // One-shot kernel: one lane per ray, all steps in one pass.
-template <bool ABS, int DEPO, bool TRAJ>
+template <int ABS, int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     AlbajarWork work = {0u, 0u, 0u};
@@ -422,11 +424,11 @@ __constant__ double c_ts_bt[7] = {-0.00178001105222577714, -0.000816434459656746
                                   0.015151515151515152};
 constexpr int kTsLds = 7 * 7 * 64;  // doubles per wave
 
-template <bool ABS>
+template <int ABS>
 __device__ __forceinline__ void rhs7(const TraceArgs &a, const double u[7], double du[7],
                                      AlbajarWork &work, unsigned long long &nrhs) {
     double al;
-    ray_rhs<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, u, u + 3, du, al, &work);
+    ray_rhs_m<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, a.abs_model, u, u + 3, du, al, &work);
     du[6] = -u[6] * al;  // sys!: du[7] = -P alpha (src/solve.jl:113)
     nrhs++;
 }
@@ -438,7 +440,7 @@ __device__ __forceinline__ double rms7(const double v[7]) {
     return sqrt(s * (1.0 / 7.0));
 }
 
-template <bool ABS, int DEPO, bool TRAJ>
+template <int ABS, int DEPO, bool TRAJ>
 __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r, int ch,
                                 double *kl, AlbajarWork &work, unsigned long long &nrhs) {
     // kl: this wave's LDS stage store, [stage][component][lane].  One RHS call
@@ -619,13 +621,15 @@ __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r
 // {tag = p + 1, group} (agent-scope release fence after the state stores, then
 // a relaxed agent store).  Pop: relaxed agent poll of the granule, then an
 // agent acquire fence before the state loads (MI355X_MICROARCH.md visibility
-// rules).  Every spin is bounded (err flag) and every wave exits once all G
-// groups have retired, so the grid always drains.
+// rules).  Every spin is bounded (err flag after 120 s without a push or a
+// retirement anywhere) and every wave exits once all G groups have retired,
+// so the grid always drains.
 struct SchedCtl {
     unsigned head, tail, finished, err;
 };
 
 constexpr unsigned kGroupExit = 0xffffffffu;
+constexpr unsigned long long kStallTicks = 120ull * 100000000ull;  // 120 s at 100 MHz
 
 // returns the group index; bit 31 set = first visit (state from x0/N0)
 __device__ __forceinline__ unsigned sched_pop(SchedCtl *ctl, unsigned long long *slots, unsigned S,
@@ -639,6 +643,11 @@ __device__ __forceinline__ unsigned sched_pop(SchedCtl *ctl, unsigned long long 
         } else {
             const unsigned long long pos = h - G;
             unsigned long long *slot = slots + (pos % S);
+            // stall watchdog: no push and no retirement anywhere in the grid for
+            // kStallTicks of the 100 MHz realtime clock (a long chunk of heavy
+            // physics is progress elsewhere, not a stall)
+            unsigned long long t_prog = __builtin_amdgcn_s_memrealtime();
+            unsigned prog = 0xffffffffu;
             for (unsigned spins = 0;; spins++) {
                 unsigned long long v = __hip_atomic_load(slot, __ATOMIC_RELAXED,
                                                          __HIP_MEMORY_SCOPE_AGENT);
@@ -651,9 +660,18 @@ __device__ __forceinline__ unsigned sched_pop(SchedCtl *ctl, unsigned long long 
                     g = ((v >> 32) == pos + 1) ? (unsigned)v : kGroupExit;
                     break;
                 }
-                if (spins > (1u << 26)) {  // bounded spin: never hang the device
-                    __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    break;
+                if ((spins & 255u) == 0) {
+                    const unsigned pr =
+                        __hip_atomic_load(&ctl->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                        __hip_atomic_load(&ctl->finished, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                    if (pr != prog) {
+                        prog = pr;
+                        t_prog = now;
+                    } else if (now - t_prog > kStallTicks) {  // never hang the device
+                        __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        break;
+                    }
                 }
                 __builtin_amdgcn_s_sleep(4);
             }
@@ -671,7 +689,7 @@ __device__ __forceinline__ void sched_publish_begin() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <bool ABS, int DEPO, bool TRAJ, int INTEG>
+template <int ABS, int DEPO, bool TRAJ, int INTEG>
 __global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
                                                                      unsigned long long *slots,
                                                                      unsigned S, int G, int cs) {
@@ -790,7 +808,7 @@ __global__ void __launch_bounds__(64) k_ray_entry(EntryArgs a) {
 // dP/ds at a ray's last saved point (every other point's alpha is the next
 // step's stage-0 RHS inside the trace kernel): P alpha_approx(x, N) from the
 // final state (src/solve.jl:171)
-template <bool ABS>
+template <int ABS>
 __global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
@@ -802,7 +820,7 @@ __global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
         x[c] = a.state[c * a.n + i];
         N[c] = a.state[(3 + c) * a.n + i];
     }
-    if constexpr (ABS) ray_rhs<true>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, x, N, du, al, nullptr);
+    if constexpr (ABS != 0) ray_rhs_m<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, a.abs_model, x, N, du, al, nullptr);
     a.smp_dpds[(size_t)k * a.n + i] = exp(-a.state[6 * a.n + i]) * al;
 }
 
@@ -941,7 +959,23 @@ struct AlbArgs {
     int n, mode;
     const double *omega, *X, *Y, *Nabs, *Npar, *Te;
     double *out;
+    const double *inv;  // warm: 1 / |dD/dN|
+    double *n2;         // warm: N_perp^2 (re, im interleaved), may be null
+    int iwarm;
 };
+
+// warm absorption alpha (torj_warm.hpp) at arbitrary points: one lane each
+__global__ void __launch_bounds__(64) k_alpha_warm(AlbArgs a) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    cplx n2;
+    a.out[i] = alpha_warm(a.omega[i], a.X[i], a.Y[i], a.Nabs[i], a.Npar[i], a.Te[i], a.inv[i],
+                          a.mode, a.iwarm, &n2);
+    if (a.n2) {
+        a.n2[2 * i] = n2.re;
+        a.n2[2 * i + 1] = n2.im;
+    }
+}
 
 __global__ void __launch_bounds__(256, 1) k_albajar(AlbArgs a) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1077,6 +1111,7 @@ struct torj_plasma_s {
     void *d_sched = nullptr;  // work-queue control block + ready-queue ring (zeroed per launch)
     size_t sched_cap = 0;
     bool last_sched = false;               // last torj_trace_device launch used the work queue
+    int last_groups = 0;                   // its number of 64-ray groups
     int sched_mode = -1, sched_waves = 0;  // torj_set_sched
     int *d_chunk = nullptr;                // integrator 1: chunks done per ray
     size_t chunk_cap = 0;
@@ -1647,6 +1682,35 @@ int torj_abs_albajar_fast(int n, const double *omega, const double *X, const dou
     return batched_scalar(true, n, omega, X, Y, Nabs, Npar, Te, mode, alpha);
 }
 
+int torj_alpha_warm(int n, const double *omega, const double *X, const double *Y,
+                    const double *Nabs, const double *Npar, const double *Te,
+                    const double *inv_dDdN, int mode, int iwarm, double *alpha, double *Nperp2) {
+    if (n <= 0) return 0;
+    if (iwarm != 1 && iwarm != 3) return fail("iwarm must be 1 or 3");
+    if (mode != 1 && mode != -1) return fail("mode must be +1 (X) or -1 (O)");
+    DevBufs B;
+    AlbArgs a{};
+    a.n = n;
+    a.mode = mode;
+    a.iwarm = iwarm;
+    double *d[9];
+    const double *h[7] = {omega, X, Y, Nabs, Npar, Te, inv_dDdN};
+    for (int k = 0; k < 7; k++) {
+        if (!h[k]) return fail("torj_alpha_warm: every input array is required");
+        if (dupload(&d[k], h[k], n, nullptr)) return -1;
+        B.track(d[k]);
+    }
+    if (dalloc(&d[7], n, true) || dalloc(&d[8], 2 * (size_t)n, true)) return -1;
+    B.track(d[7]), B.track(d[8]);
+    a.omega = d[0], a.X = d[1], a.Y = d[2], a.Nabs = d[3], a.Npar = d[4], a.Te = d[5];
+    a.inv = d[6], a.out = d[7], a.n2 = d[8];
+    hipLaunchKernelGGL(k_alpha_warm, dim3(nblocks(n, 64)), dim3(64), 0, nullptr, a);
+    HIPCK(hipGetLastError());
+    HIPCK(hipMemcpy(alpha, d[7], n * sizeof(double), hipMemcpyDeviceToHost));
+    if (Nperp2) HIPCK(hipMemcpy(Nperp2, d[8], 2 * n * sizeof(double), hipMemcpyDeviceToHost));
+    return 0;
+}
+
 int torj_refractive_index_sq(int n, const double *X, const double *Y, const double *Npar, int mode,
                              double *out) {
     return batched_scalar(false, n, nullptr, X, Y, nullptr, Npar, nullptr, mode, out);
@@ -1717,7 +1781,8 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         return fail("deposition = 1 (reference profile) needs x_launch and s0 (torj_trace_ex)");
     const bool tr = cfg->traj_stride > 0 && traj;
     if (ensure_device(p)) return -1;
-    if (cfg->absorption && ensure_gl_on_device(p->device)) return -1;
+    if (cfg->absorption < 0 || cfg->absorption > 3) return fail("absorption must be 0..3");
+    if (cfg->absorption == 1 && ensure_gl_on_device(p->device)) return -1;
     hipStream_t s = (hipStream_t)stream;
     TraceArgs a{};
     a.coef = p->d_coef;
@@ -1739,6 +1804,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     a.steps = steps;
     a.counters = (unsigned long long *)counters;
     a.s0 = s0;
+    a.abs_model = cfg->absorption;
     if (cfg->integrator == 1) {
         a.abstol = cfg->abstol;
         a.reltol = cfg->reltol;
@@ -1849,10 +1915,12 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     } while (0)
 #define TORJ_DISPATCH_TRACE(L)              \
     do {                                    \
-        if (cfg->absorption)                \
-            TORJ_DISPATCH_D(L, true);       \
+        if (cfg->absorption >= 2)           \
+            TORJ_DISPATCH_D(L, 2);          \
+        else if (cfg->absorption == 1)      \
+            TORJ_DISPATCH_D(L, 1);          \
         else                                \
-            TORJ_DISPATCH_D(L, false);      \
+            TORJ_DISPATCH_D(L, 0);          \
     } while (0)
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     if (p->timing) {
@@ -1885,6 +1953,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         HIPCK(hipMemsetAsync(p->d_sched, 0, bytes, s));
         SchedCtl *ctl = (SchedCtl *)p->d_sched;
         p->last_sched = true;
+        p->last_groups = G;
         unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
         const dim3 grd(W), blk(64);
 #define LAUNCH(A, D, T)                                                                            \
@@ -1909,10 +1978,12 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     if (fit) {
         if (adaptive)
             ;  // the last accepted step's FSAL stage already gave P alpha there
-        else if (cfg->absorption)
-            hipLaunchKernelGGL(k_final_alpha<true>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+        else if (cfg->absorption >= 2)
+            hipLaunchKernelGGL(k_final_alpha<2>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+        else if (cfg->absorption == 1)
+            hipLaunchKernelGGL(k_final_alpha<1>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         else
-            hipLaunchKernelGGL(k_final_alpha<false>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+            hipLaunchKernelGGL(k_final_alpha<0>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), 0, s, fa);
         hipLaunchKernelGGL(k_shell_sum, dim3(n_psi), dim3(256), 0, s, fa);
         HIPCK(hipGetLastError());
@@ -2019,13 +2090,18 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
         if (Pdep) std::fill(Pdep, Pdep + n, 0.0);
     }
     if (traj && n_save > 0 && ddownload(traj, dtraj, (size_t)n_save * 5 * n, s)) return -1;
-    HIPCK(hipStreamSynchronize(s));
-    if (p->last_sched) {  // bounded-spin watchdog of the work queue
+    return torj_trace_check(p, s);
+}
+
+int torj_trace_check(torj_plasma_t p, void *stream) {
+    if (!p) return fail("bad plasma handle");
+    HIPCK(hipStreamSynchronize((hipStream_t)stream));
+    if (p->last_sched) {  // stall watchdog / retirement count of the work queue
         SchedCtl ctl;
         HIPCK(hipMemcpy(&ctl, p->d_sched, sizeof(ctl), hipMemcpyDeviceToHost));
         if (ctl.err) return fail("work-queue watchdog fired (ready-queue stalled)");
-        if (ctl.finished != (unsigned)((n + 63) / 64))
-            return fail("work queue retired %u of %d ray groups", ctl.finished, (n + 63) / 64);
+        if (ctl.finished != (unsigned)p->last_groups)
+            return fail("work queue retired %u of %d ray groups", ctl.finished, p->last_groups);
     }
     return 0;
 }

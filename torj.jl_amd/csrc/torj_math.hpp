@@ -277,7 +277,7 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
 // D(x,N) and its gradients (replaces ForwardDiff in gradΛ!, src/solve.jl:85-93).
 // du = (dD/dN, -dD/dx) / |dD/dN|.
 TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode, double du[6],
-                               double *Npar_out) {
+                               double *Npar_out, double *inv_out = nullptr) {
     const double Npar = N[0] * p.b[0] + N[1] * p.b[1] + N[2] * p.b[2];
     const NsPartials ns = refractive_index_sq_partials(p.X, p.Y, Npar, mode);
     const double N2 = N[0] * N[0] + N[1] * N[1] + N[2] * N[2];
@@ -294,6 +294,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
     }
     const double nrm = sqrt(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
     const double inv = 1.0 / nrm;
+    if (inv_out) *inv_out = inv;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         du[q] = dDdN[q] * inv;

@@ -1,0 +1,561 @@
+// torj_warm.hpp -- warm-plasma EC absorption (src/general_absorption.jl,
+// GRAY's warm dispersion module), restated for the device and repaired as
+// described in oracle/warm_ref.py (R1-R5):
+//   warmdisp (:1158-1267) solves the warm dispersion relation for N_perp with
+//   the weakly relativistic tensor (iwarm 1: fsup + the plasma dispersion
+//   function, :473-638) or the fully relativistic one (iwarm 3, what the
+//   reference's alpha hard-codes: hermitian part by the 501-node t-quadrature
+//   with exp(-x) Ei(x), anti-hermitian part analytic, :646-1134); larmornumber
+//   (:1285-1326) sets the Larmor-radius order; alpha (:1328-1337) =
+//   2 Im(N_perp^2) (omega / c) v_g_perp with v_g_perp = 1 / |dD/dN|.
+// One lane evaluates one point; small tensors live in the lane's private
+// memory.  This is the heavy-VALU configuration C5 (~1e5 flop per alpha).
+#pragma once
+#include "torj_math.hpp"
+
+namespace torj {
+
+struct cplx {
+    double re, im;
+};
+TORJ_HD cplx C(double r, double i = 0.0) { return cplx{r, i}; }
+TORJ_HD cplx operator+(cplx a, cplx b) { return {a.re + b.re, a.im + b.im}; }
+TORJ_HD cplx operator-(cplx a, cplx b) { return {a.re - b.re, a.im - b.im}; }
+TORJ_HD cplx operator-(cplx a) { return {-a.re, -a.im}; }
+TORJ_HD cplx operator*(cplx a, cplx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
+TORJ_HD cplx operator*(double s, cplx a) { return {s * a.re, s * a.im}; }
+TORJ_HD cplx operator*(cplx a, double s) { return {s * a.re, s * a.im}; }
+TORJ_HD cplx operator/(cplx a, double s) { return {a.re / s, a.im / s}; }
+TORJ_HD cplx operator/(cplx a, cplx b) {  // Smith's algorithm
+    if (fabs(b.re) >= fabs(b.im)) {
+        const double r = b.im / b.re, d = b.re + b.im * r;
+        return {(a.re + a.im * r) / d, (a.im - a.re * r) / d};
+    }
+    const double r = b.re / b.im, d = b.re * r + b.im;
+    return {(a.re * r + a.im) / d, (a.im * r - a.re) / d};
+}
+TORJ_HD cplx operator+(double s, cplx a) { return {s + a.re, a.im}; }
+TORJ_HD cplx operator-(double s, cplx a) { return {s - a.re, -a.im}; }
+TORJ_HD cplx operator+(cplx a, double s) { return {a.re + s, a.im}; }
+TORJ_HD cplx operator-(cplx a, double s) { return {a.re - s, a.im}; }
+TORJ_HD cplx I_times(cplx a) { return {-a.im, a.re}; }
+TORJ_HD double cabs_(cplx a) { return hypot(a.re, a.im); }
+TORJ_HD cplx csqrt_(cplx z) {  // principal branch, as Julia's sqrt(::ComplexF64)
+    if (z.re == 0.0 && z.im == 0.0) return {0.0, z.im};
+    const double r = cabs_(z);
+    double t = sqrt(0.5 * (r + fabs(z.re)));
+    if (z.re >= 0.0) return {t, 0.5 * z.im / t};
+    return {0.5 * fabs(z.im) / t, copysign(t, z.im)};
+}
+
+constexpr double kSqrtPi = 1.7724538509055160272981674833411;
+constexpr double kEulerGamma = 0.57721566490153286060651209008240243;
+constexpr int kWarmMaxL = 5;  // i_max (src/constants.jl:4)
+constexpr int kNtv = 501;     // t-quadrature (src/constants.jl:1-3)
+constexpr double kTmax = 5.0, kDtv = 2.0 * kTmax / (kNtv - 1);
+
+// exp(-x) Ei(x) (calcei int = 3, :29-232), restated: power series of Ei / E1
+// near 0, continued fraction for e^y E1(y) (y > 1), asymptotic series for
+// |x| >= 40.  -1.79e308 at x = 0 (the reference's -xinf).
+TORJ_HD double expei(double x) {
+    if (x == 0.0) return -1.79e308;
+    const double ax = fabs(x);
+    if (ax >= 40.0) {  // e^-x Ei(x) ~ (1/x) sum_k k!/x^k (both signs)
+        double s = 1.0, term = 1.0;
+        for (int k = 1; k < 40; k++) {
+            const double nt = term * k / x;
+            if (fabs(nt) >= fabs(term)) break;  // optimal truncation
+            term = nt;
+            s += term;
+            if (fabs(term) < 1e-17 * fabs(s)) break;
+        }
+        return s / x;
+    }
+    if (x < 0.0) {
+        const double y = -x;
+        if (y <= 1.0) {  // E1(y) = -gamma - ln y - sum (-y)^k / (k k!)
+            double s = 0.0, term = 1.0;
+            for (int k = 1; k <= 24; k++) {
+                term *= -y / k;
+                s += term / k;
+            }
+            const double E1 = -kEulerGamma - log(y) - s;
+            return -exp(y) * E1;
+        }
+        // e^y E1(y) = 1 / (y + 1 - 1 / (y + 3 - 4 / (y + 5 - ...))), modified Lentz
+        const double tiny = 1e-300;
+        double b = y + 1.0, c = 1.0 / tiny, d = 1.0 / b, h = d;
+        for (int k = 1; k < 300; k++) {
+            const double an = -(double)k * k;
+            b += 2.0;
+            d = 1.0 / (an * d + b);
+            c = b + an / c;
+            const double del = c * d;
+            h *= del;
+            if (fabs(del - 1.0) < 1e-16) break;
+        }
+        return -h;  // e^-x Ei(x) = -e^y E1(y)
+    }
+    // 0 < x < 40: Ei(x) = gamma + ln x + sum x^k / (k k!)
+    double s = 0.0, term = 1.0;
+    for (int k = 1; k < 200; k++) {
+        term *= x / k;
+        const double add = term / k;
+        s += add;
+        if (add < 1e-17 * s) break;
+    }
+    return exp(-x) * (kEulerGamma + log(x) + s);
+}
+
+TORJ_HD double factd(int k) {
+    double f = 1.0;
+    for (int i = 2; i <= k; i++) f *= (double)i;
+    return k < 0 ? 0.0 : f;
+}
+
+// Numerical Recipes lnGamma, the reference's gammln (:265-283)
+TORJ_HD double gammln_nr(double x) {
+    const double cof[6] = {76.18009172947146,     -86.50532032941677, 24.01409824083091,
+                           -1.231739572450155,    0.1208650973866179e-2, -0.5395239384953e-5};
+    double y = x, tmp = x + 5.5;
+    tmp = (x + 0.5) * log(tmp) - tmp;
+    double ser = 1.000000000190015;
+    for (int j = 0; j < 6; j++) {
+        y += 1.0;
+        ser += cof[j] / y;
+    }
+    return tmp + log(2.5066282746310005 * ser / x);
+}
+
+// I_{m+1/2}(z)/(z/2)^{m+1/2} series for m = n .. l+2 (ssbi, :291-320, R1)
+TORJ_HD void ssbi(double zz, int n, int l, double out[kWarmMaxL + 3]) {
+    const double z2q = 0.25 * zz * zz;
+    for (int m = n; m <= l + 2; m++) {
+        double c0 = 1.0 / exp(gammln_nr(m + 1.5)), s = c0;
+        for (int k = 1; k <= 50; k++) {
+            const double c1 = c0 * z2q / ((m + k) + 0.5) / k;
+            s += c1;
+            if (c1 / s < 1e-10) break;
+            c0 = c1;
+        }
+        out[m - n] = s;
+    }
+}
+
+// Faddeeva w(z) for Z(z) = i sqrt(pi) w(z) (zetac, :345-465): Poppe & Wijers,
+// ACM TOMS 680 (series near the origin, Laplace continued fraction / truncated
+// Taylor expansion otherwise, reflection for Im z < 0)
+TORJ_HD cplx faddeeva(double xi, double yi) {
+    const double factor = 1.12837916709551257388;  // 2/sqrt(pi)
+    const double xabs = fabs(xi), yabs = fabs(yi);
+    const double x = xabs / 6.3, y = yabs / 4.4;
+    double qrho = x * x + y * y;
+    const double xquad = xabs * xabs - yabs * yabs, yquad = 2.0 * xabs * yabs;
+    double u, v, u2 = 0.0, v2 = 0.0;
+    const bool small = qrho < 0.085264;
+    if (small) {
+        qrho = (1.0 - 0.85 * y) * sqrt(qrho);
+        const int n = (int)rint(6.0 + 72.0 * qrho);
+        int j = 2 * n + 1;
+        double xsum = 1.0 / j, ysum = 0.0;
+        for (int i = n; i >= 1; i--) {
+            j -= 2;
+            const double xaux = (xsum * xquad - ysum * yquad) / i;
+            ysum = (xsum * yquad + ysum * xquad) / i;
+            xsum = xaux + 1.0 / j;
+        }
+        const double u1 = -factor * (xsum * yabs + ysum * xabs) + 1.0;
+        const double v1 = factor * (xsum * xabs - ysum * yabs);
+        const double daux = exp(-xquad);
+        u2 = daux * cos(yquad);
+        v2 = -daux * sin(yquad);
+        u = u1 * u2 - v1 * v2;
+        v = u1 * v2 + v1 * u2;
+    } else {
+        double h = 0.0, h2 = 0.0;
+        int kapn = 0, nu;
+        if (qrho > 1.0) {
+            qrho = sqrt(qrho);
+            nu = 3 + (int)floor(1442.0 / (26.0 * qrho + 77.0));
+        } else {
+            qrho = (1.0 - y) * sqrt(1.0 - qrho);
+            h = 1.88 * qrho;
+            h2 = 2.0 * h;
+            kapn = (int)rint(7.0 + 34.0 * qrho);
+            nu = (int)rint(16.0 + 26.0 * qrho);
+        }
+        double qlambda = h > 0.0 ? pow(h2, (double)kapn) : 0.0;
+        double rx = 0.0, ry = 0.0, sx = 0.0, sy = 0.0;
+        for (int n = nu; n >= 0; n--) {
+            const double np1 = n + 1.0;
+            double tx = yabs + h + np1 * rx, ty = xabs - np1 * ry;
+            const double c = 0.5 / (tx * tx + ty * ty);
+            rx = c * tx;
+            ry = c * ty;
+            if (h > 0.0 && n <= kapn) {
+                tx = qlambda + sx;
+                sx = rx * tx - ry * sy;
+                sy = ry * tx + rx * sy;
+                qlambda /= h2;
+            }
+        }
+        if (h == 0.0) {
+            u = factor * rx;
+            v = factor * ry;
+        } else {
+            u = factor * sx;
+            v = factor * sy;
+        }
+        if (yabs == 0.0) u = exp(-xabs * xabs);
+    }
+    if (yi < 0.0) {
+        if (small) {
+            u2 *= 2.0;
+            v2 *= 2.0;
+        } else {
+            const double w1 = 2.0 * exp(-xquad);
+            u2 = w1 * cos(yquad);
+            v2 = -w1 * sin(yquad);
+        }
+        u = u2 - u;
+        v = v2 - v;
+        if (xi > 0.0) v = -v;
+    } else if (xi < 0.0) {
+        v = -v;
+    }
+    return {u, v};
+}
+TORJ_HD cplx zetac(double x, double y) {
+    const cplx w = faddeeva(x, y);
+    return {-kSqrtPi * w.im, kSqrtPi * w.re};
+}
+
+struct Tensor {  // epsl(3,3,lrm) upper triangle (11 12 22 13 23 33) + e330
+    cplx e[kWarmMaxL][6];
+    cplx e330;
+};
+
+// the l-sum of the tensor (shared by both models): fl, ca -> epsl(:,:,l)
+TORJ_HD void tensor_store(Tensor &T, int l, double xg, double fl, const cplx ca[6]) {
+    T.e[l - 1][0] = -xg * ca[0] * fl;
+    T.e[l - 1][1] = I_times(xg * ca[1] * fl);
+    T.e[l - 1][2] = -xg * ca[2] * fl;
+    T.e[l - 1][3] = -xg * ca[3] * fl;
+    T.e[l - 1][4] = -I_times(xg * ca[4] * fl);
+    T.e[l - 1][5] = -xg * ca[5] * fl;
+}
+
+// weakly relativistic tensor (fsup + dieltens_maxw_wr, :473-638)
+TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor &T) {
+    cplx cefp[kWarmMaxL + 1][3], cefm[kWarmMaxL + 1][3];
+    for (int a = 0; a <= lrm; a++)
+        for (int b = 0; b < 3; b++) cefp[a][b] = cefm[a][b] = C(0.0);
+    const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
+    for (int is = -lrm; is <= lrm; is++) {
+        const double alpha = anpl2hm1 + is * yg, phi2 = amu * alpha, phim = sqrt(fabs(phi2));
+        double xp, yp, xm, ym, x0, y0;
+        if (alpha >= 0) {
+            xp = psi - phim, yp = 0.0, xm = -psi - phim, ym = 0.0, x0 = -phim, y0 = 0.0;
+        } else {
+            xp = psi, yp = phim, xm = -psi, ym = phim, x0 = 0.0, y0 = phim;
+        }
+        const cplx czp = zetac(xp, yp), czm = zetac(xm, ym);
+        cplx cf12 = C(0.0);
+        if (alpha > 0)
+            cf12 = -(czp + czm) / (2.0 * phim);
+        else if (alpha < 0)
+            cf12 = -I_times((czp + czm) / (2.0 * phim));
+        cplx cf32;
+        if (apsi > 0.7) {
+            cf32 = -(czp - czm) / (2.0 * psi);
+        } else {
+            const cplx cphi = alpha < 0 ? C(0.0, -phim) : C(phim);
+            cf32 = 2.0 * (1.0 - cphi * zetac(x0, y0));
+        }
+        cplx cf0 = cf12, cf1 = cf32;
+        if (is == 0) cefp[0][0] = cefm[0][0] = cf32;
+        const int isa = abs(is);
+        for (int l = 1; l <= isa + 2; l++) {
+            const cplx cf2 = apsi > 0.7 ? (1.0 + phi2 * cf0 - (l - 0.5) * cf1) / (psi * psi)
+                                         : (1.0 + phi2 * cf1) / (l + 0.5);
+            const int ir = l - isa;
+            if (ir >= 0) {
+                cefp[isa][ir] = cefp[isa][ir] + cf2;
+                cefm[isa][ir] = is > 0 ? cefm[isa][ir] + cf2 : cefm[isa][ir] - cf2;
+            }
+            cf0 = cf1;
+            cf1 = cf2;
+        }
+    }
+    const double anpl2 = anpl * anpl;
+    for (int l = 1; l <= lrm; l++) {
+        const int lm = l - 1;
+        const double fcl = pow(0.5, l) * pow((1.0 / yg) * (1.0 / yg) / amu, lm) * factd(2 * l) / factd(l);
+        cplx ca[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
+        for (int is = 0; is <= l; is++) {
+            const int k = l - is;
+            const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(is + l) * factd(l - is));
+            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + is)) / (2 * l - 1));
+            const cplx cq0p = amu * cefp[is][0], cq0m = amu * cefm[is][0];
+            const cplx cq1p = amu * anpl * (cefp[is][0] - cefp[is][1]);
+            const cplx cq1m = amu * anpl * (cefm[is][0] - cefm[is][1]);
+            const cplx cq2p = cefp[is][1] + amu * anpl2 * (cefp[is][2] + cefp[is][0] - 2.0 * cefp[is][1]);
+            ca[0] = ca[0] + (double)(is * is) * asl * cq0p;
+            ca[1] = ca[1] + (double)(is * l) * asl * cq0m;
+            ca[2] = ca[2] + bsl * cq0p;
+            ca[3] = ca[3] + (double)is * asl * cq1m / yg;
+            ca[4] = ca[4] + (double)l * asl * cq1p / yg;
+            ca[5] = ca[5] + asl * cq2p / (yg * yg);
+        }
+        tensor_store(T, l, xg, fcl, ca);
+    }
+    const cplx cq2p = cefp[0][1] + amu * anpl2 * (cefp[0][2] + cefp[0][0] - 2.0 * cefp[0][1]);
+    T.e330 = 1.0 - xg * amu * cq2p;
+}
+
+// fully relativistic tensor (hermitian iwarm > 2 + antihermitian +
+// dieltens_maxw_fr, :646-1134)
+TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm, Tensor &T) {
+    const int llm = lrm < 3 ? lrm : 3;
+    // rr[n + 3][k][m], n in [-llm, llm], m in [|n|, llm]
+    double rr[7][3][4];
+    for (int a = 0; a < 7; a++)
+        for (int b = 0; b < 3; b++)
+            for (int c = 0; c < 4; c++) rr[a][b][c] = 0.0;
+    const double cmxw = 1.0 + 15.0 / (8.0 * amu) + 105.0 / (128.0 * amu * amu);
+    const double cr = -amu * amu / (kSqrtPi * cmxw);
+    const double bth2 = 2.0 / amu, bth = sqrt(bth2);
+    const double amu2 = amu * amu, amu4 = amu2 * amu2, amu6 = amu4 * amu2;
+    for (int n = -llm; n <= llm; n++) {
+        const int mlo = n < 0 ? -n : n;
+        double acc[4][3];
+        for (int m = 0; m < 4; m++) acc[m][0] = acc[m][1] = acc[m][2] = 0.0;
+        for (int i = 0; i < kNtv; i++) {
+            const double t = -kTmax + i * kDtv;
+            const double rxt = sqrt(1.0 + t * t / (2.0 * amu)), x = t * rxt;
+            const double upl2 = bth2 * x * x, upl = bth * x, gx = 1.0 + t * t / amu;
+            const double exdx = cr * (exp(-t * t) * kDtv) * gx / rxt;
+            const double gr = anpl * upl + n * yg;
+            const double zm = -amu * (gx - gr), s = amu * (gx + gr);
+            const double fe0m = expei(zm), zm2 = zm * zm;
+            for (int m = mlo; m <= llm; m++) {
+                if (m == 0) {
+                    acc[0][2] += -exdx * fe0m * upl2;
+                    continue;
+                }
+                double ffe;
+                if (m == 1)
+                    ffe = (1.0 + s * (1.0 - zm * fe0m)) / amu2;
+                else if (m == 2)
+                    ffe = (6.0 - 2.0 * zm + 4.0 * s + s * s * (1.0 + zm - zm2 * fe0m)) / amu4;
+                else
+                    ffe = (18.0 * s * (s + 4.0 - zm) + 6.0 * (20.0 - 8.0 * zm + zm2) +
+                           s * s * s * (2.0 + zm + zm2 - zm2 * zm * fe0m)) / amu6;
+                acc[m][0] += exdx * ffe;
+                acc[m][1] += exdx * ffe * upl;
+                acc[m][2] += exdx * ffe * upl2;
+            }
+        }
+        for (int m = mlo; m <= llm; m++)
+            for (int k = 0; k < 3; k++) rr[n + 3][k][m] = acc[m][k];
+    }
+    // anti-hermitian part ri[n-1][k][m-1], m >= n
+    double ri[kWarmMaxL][3][kWarmMaxL];
+    for (int a = 0; a < kWarmMaxL; a++)
+        for (int b = 0; b < 3; b++)
+            for (int c = 0; c < kWarmMaxL; c++) ri[a][b][c] = 0.0;
+    const double dnl = 1.0 - anpl * anpl, cmu = anpl * amu;
+    const double ci = sqrt(2.0 * kPi * amu) * amu * amu / cmxw;
+    for (int n = 1; n <= lrm; n++) {
+        const double ygn = n * yg, rdu2 = ygn * ygn - dnl;
+        if (!(rdu2 > 0.0)) continue;
+        const double du = sqrt(rdu2) / dnl, ub = anpl * ygn / dnl, aa = amu * anpl * du;
+        if (fabs(aa) > 5.0) {
+            const double up = ub + du, um = ub - du;
+            const double gp = anpl * up + ygn, gm = anpl * um + ygn;
+            const double xp = up + 1.0 / cmu, xm = um + 1.0 / cmu;
+            const double eem = exp(-amu * (gm - 1.0)), eep = exp(-amu * (gp - 1.0));
+            double f0p = -1.0 / cmu, f1p = -xp / cmu, f2p = -(1.0 / (cmu * cmu) + xp * xp) / cmu;
+            double f0m = -1.0 / cmu, f1m = -xm / cmu, f2m = -(1.0 / (cmu * cmu) + xm * xm) / cmu;
+            for (int m = 1; m <= lrm; m++) {
+                const double g0p = -2.0 * m * (f1p - ub * f0p) / cmu;
+                const double g0m = -2.0 * m * (f1m - ub * f0m) / cmu;
+                const double g1p = -((1.0 + 2 * m) * f2p - 2.0 * (m + 1) * ub * f1p + up * um * f0p) / cmu;
+                const double g1m = -((1.0 + 2 * m) * f2m - 2.0 * (m + 1) * ub * f1m + up * um * f0m) / cmu;
+                const double g2p = (2.0 * (1 + m) * g1p - 2.0 * m * (ub * f2p - up * um * f1p)) / cmu;
+                const double g2m = (2.0 * (1 + m) * g1m - 2.0 * m * (ub * f2m - up * um * f1m)) / cmu;
+                if (m >= n) {
+                    const double h = 0.5 * ci * pow(dnl, m);
+                    ri[n - 1][0][m - 1] = h * (g0p * eep - g0m * eem);
+                    ri[n - 1][1][m - 1] = h * (g1p * eep - g1m * eem);
+                    ri[n - 1][2][m - 1] = h * (g2p * eep - g2m * eem);
+                }
+                f0p = g0p, f1p = g1p, f2p = g2p, f0m = g0m, f1m = g1m, f2m = g2m;
+            }
+        } else {
+            const double ee = exp(-amu * (ygn - 1.0 + anpl * ub));
+            double fsbi[kWarmMaxL + 3];
+            ssbi(aa, n, lrm, fsbi);
+            for (int m = n; m <= lrm; m++) {
+                const double cm = kSqrtPi * factd(m) * pow(du, 2 * m + 1);
+                const double cim = 0.5 * ci * pow(dnl, m);
+                const int mm = m - n;
+                const double fi0 = cm * fsbi[mm], fi1 = -0.5 * aa * cm * fsbi[mm + 1];
+                const double fi2 = 0.5 * cm * (fsbi[mm + 1] + 0.5 * aa * aa * fsbi[mm + 2]);
+                ri[n - 1][0][m - 1] = cim * ee * fi0;
+                ri[n - 1][1][m - 1] = cim * ee * (du * fi1 + ub * fi0);
+                ri[n - 1][2][m - 1] = cim * ee * (du * du * fi2 + 2.0 * du * ub * fi1 + ub * ub * fi0);
+            }
+        }
+    }
+    // rr is only populated for |n| <= llm <= 3 and m <= llm (the reference's
+    // rr(n,k,m) with m > llm stays 0): read through a guard
+    auto RR = [&](int n, int k, int m) -> double {
+        return (n >= -3 && n <= 3 && m <= 3) ? rr[n + 3][k][m] : 0.0;
+    };
+    for (int l = 1; l <= lrm; l++) {
+        const int lm = l - 1;
+        const double fal = -pow(0.25, l) * factd(2 * l) / (factd(l) * factd(l) * pow(yg, 2 * lm));
+        cplx ca[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
+        for (int is = 0; is <= l; is++) {
+            const int k = l - is;
+            const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(is + l) * factd(l - is));
+            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + is)) / (2 * l - 1));
+            cplx cq0p, cq0m, cq1p, cq1m, cq2p;
+            if (is > 0) {
+                cq0p = C(RR(is, 0, l) + RR(-is, 0, l), ri[is - 1][0][l - 1]);
+                cq0m = C(RR(is, 0, l) - RR(-is, 0, l), ri[is - 1][0][l - 1]);
+                cq1p = C(RR(is, 1, l) + RR(-is, 1, l), ri[is - 1][1][l - 1]);
+                cq1m = C(RR(is, 1, l) - RR(-is, 1, l), ri[is - 1][1][l - 1]);
+                cq2p = C(RR(is, 2, l) + RR(-is, 2, l), ri[is - 1][2][l - 1]);
+            } else {
+                cq0p = cq0m = C(RR(0, 0, l));
+                cq1p = cq1m = C(RR(0, 1, l));
+                cq2p = C(RR(0, 2, l));
+            }
+            ca[0] = ca[0] + (double)(is * is) * asl * cq0p;
+            ca[1] = ca[1] + (double)(is * l) * asl * cq0m;
+            ca[2] = ca[2] + bsl * cq0p;
+            ca[3] = ca[3] + (double)is * asl * cq1m / yg;
+            ca[4] = ca[4] + (double)l * asl * cq1p / yg;
+            ca[5] = ca[5] + asl * cq2p / (yg * yg);
+        }
+        tensor_store(T, l, xg, fal, ca);
+    }
+    T.e330 = C(1.0 + xg * rr[3][2][0]);
+}
+
+// warmdisp (:1158-1267) -> N_perp^2 (complex); anpr2 initialised (R2)
+TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int sox, int lrm,
+                          const Tensor &T) {
+    cplx anpr2a = C(anprc * anprc), anpr2 = anpr2a;
+    const double anpl2 = anpl * anpl;
+    double errnpr = 1.0;
+    for (int i = 1; i <= 100; i++) {
+        cplx s[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
+        cplx pw = C(1.0);
+        for (int l = 0; l < lrm; l++) {
+            for (int q = 0; q < 6; q++) s[q] = s[q] + T.e[l][q] * pw;
+            pw = pw * anpr2a;
+        }
+        // diagonal identity terms for l = 1 are already in T.e[0]
+        const cplx e11 = s[0], e12 = s[1], e22 = s[2], a13 = s[3], a23 = s[4], a33 = s[5];
+        const cplx a31 = a13, a32 = -a23;
+        if (i > 2 && errnpr < 1.0e-4) break;
+        const cplx cc4 = (e11 - anpl2) * (1.0 - a33) + (a13 + anpl) * (a31 + anpl);
+        const cplx cc2 = -e12 * e12 * (1.0 - a33) - a32 * e12 * (a13 + anpl) + a23 * e12 * (a31 + anpl) -
+                         (a23 * a32 + T.e330 + (e22 - anpl2) * (1.0 - a33)) * (e11 - anpl2) -
+                         (a13 + anpl) * (a31 + anpl) * (e22 - anpl2);
+        const cplx cc0 = T.e330 * ((e11 - anpl2) * (e22 - anpl2) + e12 * e12);
+        const cplx rr = cc2 * cc2 - 4.0 * cc0 * cc4;
+        double sg;
+        if (yg > 1.0) {
+            sg = (double)sox;
+            if (rr.im <= 0.0) sg = -sg;
+        } else {
+            sg = (double)(-sox);
+            if (rr.re <= 0.0 && rr.im >= 0.0) sg = -sg;
+        }
+        anpr2 = (-cc2 + sg * csqrt_(rr)) / (2.0 * cc4);
+        errnpr = fabs(1.0 - cabs_(anpr2) / cabs_(anpr2a));
+        anpr2a = anpr2;
+    }
+    if (anpr2.re < 0.0 && anpr2.im < 0.0) anpr2 = C(0.0);  // ierr = 99
+    return anpr2;
+}
+
+// larmornumber (:1285-1326)
+TORJ_HD int larmornumber(double yg, double npl, double mu) {
+    const double dnl = 1.0 - npl * npl;
+    int imax = 1;
+    int nharm = (int)floor(1.0 / yg);
+    if (nharm * yg < 1.0) nharm++;
+    for (;;) {
+        const double ygn = nharm * yg, rdu2 = ygn * ygn - dnl;
+        const double gg = (ygn - sqrt(npl * npl * rdu2)) / dnl;
+        if (mu * (gg - 1.0) > 15.0) break;
+        nharm++;
+        imax++;
+        if (imax > 100) {
+            nharm = (int)floor(yg);
+            break;
+        }
+    }
+    return nharm;
+}
+
+// alpha (:1328-1337): iwarm 1 (weakly relativistic) or 3 (fully relativistic,
+// the reference's choice); inv_dDdN = 1 / |dD/dN| (R4); sox from mode (R5).
+// Returns alpha [1/m]; N_perp^2 (warm) in *n2 if given.
+// Inlined into its callers.  A noinline device build (ROCm 7.2, gfx950; -O3
+// and -O1 alike) returned the anti-hermitian part ~1e-10 of its value for some
+// inputs while the same source is exact on the host and when inlined, and a
+// printf inside the loop made it exact again: codegen-dependent, not isolated
+// further.  tests/test_gpu_warm.py pins the device result to the oracle.
+#ifndef TORJ_WARM_ATTR
+#define TORJ_WARM_ATTR TORJ_HD
+#endif
+TORJ_WARM_ATTR double alpha_warm(double omega, double X, double Y, double N_abs, double N_par,
+                                 double Te, double inv_dDdN, int mode, int iwarm, cplx *n2) {
+    const double mu = kMe * kC * kC / (Te * kE);
+    const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
+    const int nharm = larmornumber(Y, N_par, mu);
+    const int lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
+    Tensor T;
+    if (iwarm == 1)
+        dieltens_wr(X, Y, N_par, mu, lrm, T);
+    else
+        dieltens_fr(X, Y, N_par, mu, lrm, T);
+    // identity on the l = 1 diagonal (:629-630 / :1125-1126)
+    T.e[0][0] = T.e[0][0] + 1.0;
+    T.e[0][2] = T.e[0][2] + 1.0;
+    const int sox = Y <= 1.0 ? mode : -mode;
+    const cplx a2 = warmdisp_n2(X, Y, N_par, npr, sox, lrm, T);
+    if (n2) *n2 = a2;
+    return 2.0 * a2.im * omega / kC * inv_dDdN;
+}
+
+// one RHS evaluation: ABS 0 cold, 1 Albajar (abs_Albajar_fast), 2 warm with
+// iwarm = 1 (model 2, weakly relativistic) or 3 (model 3, fully relativistic);
+// separate instances keep the warm module's private frame out of the others
+template <int ABS>
+TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Consts &k,
+                       const GLTable &gl, double omega, int mode, int model, const double x[3],
+                       const double N[3], double du[6], double &alpha, AlbajarWork *work) {
+    PlasmaPoint p;
+    plasma_point<(ABS != 0)>(coef, g, k, x, p);
+    double Npar, inv;
+    dispersion_grad(p, N, mode, du, &Npar, &inv);
+    if constexpr (ABS == 1) {
+        const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
+    } else if constexpr (ABS == 2) {
+        const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+        alpha = alpha_warm(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode, model == 2 ? 1 : 3,
+                           nullptr);
+    } else {
+        alpha = 0.0;
+    }
+}
+
+}  // namespace torj

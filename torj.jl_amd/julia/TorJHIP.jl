@@ -22,7 +22,7 @@ struct TraceCfg              # torj_trace_cfg
     chunk_steps::Cint
     psi_exit::Float64
     P_min::Float64
-    absorption::Cint
+    absorption::Cint         # 0 none, 1 abs_Albajar_fast, 2 / 3 warm alpha (iwarm 1 / 3)
     traj_stride::Cint
     deposition::Cint         # 0: binned, 1: power_deposition_profile (src/plasma.jl:91-151)
     integrator::Cint         # 0: fixed RK4; 1: the reference's adaptive solve() (Tsit5)
@@ -97,14 +97,14 @@ end
 """make_ray -- same signature and return tuple as TorJ.make_ray (src/solve.jl:135-181)."""
 function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f::Real,
                   mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4,
-                  deposition::Integer=1, integrator::Integer=0)
+                  deposition::Integer=1, integrator::Integer=0, absorption::Integer=1)
     ω = 2π * f
     xp, Np, s0, st = ray_entry(p, reshape(collect(Float64, x0), 1, 3),
                                reshape(collect(Float64, N_vacuum), 1, 3), ω, mode)
     st[1] == 0 || throw(AssertionError("ray entry failed (status $(st[1]))"))
     n_steps = max(1, round(Int, s_max / ds))
     cap = integrator == 1 ? 2n_steps + 400 : n_steps
-    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition,
+    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, absorption, 1, deposition,
                    integrator, 1e-6, 1e-6, s_max, 100)
     g = collect(Float64, psi_dP_dV)
     xl = reshape(collect(Float64, x0), 1, 3)
@@ -124,7 +124,7 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
                    s_max::Float64, psi_dP_dV::Vector{Float64}; ds::Float64=1e-4,
                    N_rings::Integer=3, min_azimuthal_points::Integer=5,
                    normalize_weight_sum::Bool=true, deposition::Integer=1,
-                   integrator::Integer=0)
+                   integrator::Integer=0, absorption::Integer=1)
     N0 = zeros(3)
     ccall((:torj_pol_tor_angles_2_vector, libtorj), Cvoid, (Float64, Float64, Ptr{Float64}),
           pol, tor, N0)
@@ -147,7 +147,7 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     all(st .== 0) || throw(AssertionError("ray entry failed for $(count(st .!= 0)) rays"))
     n_steps = max(1, round(Int, s_max / ds))
     cap = integrator == 1 ? 2n_steps + 400 : n_steps
-    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, 1, 1, deposition,
+    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, absorption, 1, deposition,
                    integrator, 1e-6, 1e-6, s_max, 100)
     state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0)
     dP_dV = zeros(length(psi_dP_dV))

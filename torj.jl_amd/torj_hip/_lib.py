@@ -60,6 +60,7 @@ _SIGS = {
     "torj_dispersion": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp, C.c_double, C.c_int, _dp, _dp,
                                   _dp]),
     "torj_abs_albajar_fast": (C.c_int, [C.c_int, _dp, _dp, _dp, _dp, _dp, _dp, C.c_int, _dp]),
+    "torj_alpha_warm": (C.c_int, [C.c_int] + [_dp] * 7 + [C.c_int, C.c_int, _dp, _dp]),
     "torj_refractive_index_sq": (C.c_int, [C.c_int, _dp, _dp, _dp, C.c_int, _dp]),
     "torj_pol_tor_angles_2_vector": (None, [C.c_double, C.c_double, _dp]),
     "torj_launch_peripheral_rays": (C.c_int, [_dp, _dp, C.c_double, C.c_double, C.c_double,
@@ -76,6 +77,7 @@ _SIGS = {
     "torj_trace_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                                 _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
+    "torj_trace_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "torj_timing_read": (C.c_int, [C.c_void_p, _ip, _dp, _dp]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,

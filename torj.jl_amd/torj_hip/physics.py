@@ -24,6 +24,24 @@ def abs_Albajar_fast(omega, X, Y, N_abs, N_par, Te, mode: int):
     return float(out[0]) if scalar else out
 
 
+def alpha_warm(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode: int, iwarm: int = 3):
+    """Warm-plasma absorption coefficient alpha (src/general_absorption.jl:1328-1337, the
+    repaired module -- DESIGN.md section C5): iwarm 1 weakly relativistic, 3 fully
+    relativistic; inv_dDdN = 1 / |dD/dN| of the cold ray Hamiltonian.
+    Returns (alpha [1/m], N_perp^2) with N_perp^2 the complex warm root."""
+    scalar = np.ndim(X) == 0
+    arrs = np.broadcast_arrays(*[np.atleast_1d(f64(a))
+                                 for a in (omega, X, Y, N_abs, N_par, Te, inv_dDdN)])
+    arrs = [np.ascontiguousarray(a) for a in arrs]
+    n = len(arrs[0])
+    out = np.zeros(n)
+    npr = np.zeros(2 * n)
+    check(lib().torj_alpha_warm(n, *[dptr(a) for a in arrs], int(mode), int(iwarm), dptr(out),
+                                dptr(npr)))
+    n2 = npr[0::2] + 1j * npr[1::2]
+    return (float(out[0]), complex(n2[0])) if scalar else (out, n2)
+
+
 def refractive_index_sq(X, Y, N_par, mode: int):
     """refractive_index_sq(X, Y, N_par, mode) (src/dispersion.jl:29-32)."""
     scalar = np.ndim(X) == 0

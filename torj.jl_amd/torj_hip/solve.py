@@ -56,11 +56,25 @@ class TraceResult:
 
 DEPOSITION = {"binned": 0, "reference": 1}
 INTEGRATOR = {"rk4": 0, "adaptive": 1}
+ABSORPTION = {"none": 0, "albajar": 1, "warm_wr": 2, "warm_fr": 3}
+
+
+def _absorption_code(absorption) -> int:
+    """bool (True = Albajar, the reference's abs_Albajar_fast), a name from
+    ABSORPTION, or the ABI integer 0..3."""
+    if isinstance(absorption, str):
+        return ABSORPTION[absorption]
+    if isinstance(absorption, (bool, np.bool_)):
+        return int(bool(absorption))
+    a = int(absorption)
+    if a not in (0, 1, 2, 3):
+        raise ValueError(f"absorption must be 0..3, got {a}")
+    return a
 
 
 def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps: int,
           chunk_steps: int | None = None, psi_exit: float = 1.0, P_min: float = 1e-6,
-          absorption: bool = True, psi_grid=None, weights=None, traj_stride: int = 0,
+          absorption=True, psi_grid=None, weights=None, traj_stride: int = 0,
           deposition: str = "binned", x_launch=None, s0=None, integrator: str = "rk4",
           abstol: float = 1e-6, reltol: float = 1e-6, s_max: float | None = None,
           n_chunks: int = 100) -> TraceResult:
@@ -82,7 +96,7 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
     dmode = DEPOSITION[deposition]
     imode = INTEGRATOR[integrator]
     cfg = TraceCfg(float(omega), int(mode), float(ds), int(n_steps), int(chunk_steps),
-                   float(psi_exit), float(P_min), int(bool(absorption)), int(traj_stride), dmode,
+                   float(psi_exit), float(P_min), _absorption_code(absorption), int(traj_stride), dmode,
                    imode, float(abstol), float(reltol),
                    float(s_max if s_max is not None else n_steps * ds), int(n_chunks))
     xl = soa(x_launch) if x_launch is not None else None
@@ -110,11 +124,13 @@ def _steps_for(s_max: float, ds: float) -> int:
 
 def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV, *,
              ds: float = 1e-4, deposition: str = "reference", integrator: str = "rk4",
-             max_steps: int | None = None):
+             max_steps: int | None = None, absorption="albajar"):
     """make_ray (src/solve.jl:135-181) -> (s, u, P_beam, dP_dV_ray, deposited_power).
     deposition="reference" (default) follows power_deposition_profile; "binned"
     uses the in-kernel shell binning.  integrator="adaptive" runs the reference's
-    solve() semantics (Tsit5, dtmax = ds, 100 chunks); "rk4" fixed steps of ds."""
+    solve() semantics (Tsit5, dtmax = ds, 100 chunks); "rk4" fixed steps of ds.
+    absorption: "albajar" (alpha_approx, the reference's), "warm_wr" / "warm_fr"
+    (general_absorption.jl's alpha, iwarm 1 / 3) or "none"."""
     omega = 2.0 * np.pi * f
     x0 = f64(x0)
     xp, Np, s0, st = ray_entry(plasma, x0[None], f64(N_vacuum)[None], omega, mode)
@@ -125,7 +141,8 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
         n_steps = max_steps or 2 * n_steps + 400
     g = f64(psi_dP_dV)
     r = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, traj_stride=1,
-              deposition=deposition, x_launch=x0[None], s0=s0, integrator=integrator, s_max=s_max)
+              deposition=deposition, x_launch=x0[None], s0=s0, integrator=integrator, s_max=s_max,
+              absorption=absorption)
     if r.status[0] == MAX_STEPS:
         raise RuntimeError("make_ray: accepted-step capacity exhausted (raise max_steps)")
     k = int(r.steps[0])
@@ -142,7 +159,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
               steering_angle_pol: float, spot_size: float, inverse_curvature_radius: float,
               f: float, mode: int, s_max: float, psi_dP_dV, *, ds: float = 1e-4,
               traj_stride: int = 1, deposition: str = "reference", integrator: str = "rk4",
-              max_steps: int | None = None, **kwargs):
+              max_steps: int | None = None, absorption="albajar", **kwargs):
     """make_beam (src/solve.jl:209-242) -> (arc_lengths, trajectories, ray_powers, dP_dV,
     deposited_power, ray_weights).  kwargs go to launch_peripheral_rays."""
     omega = 2.0 * np.pi * f
@@ -160,7 +177,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     g = f64(psi_dP_dV)
     res = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, weights=w,
                 traj_stride=traj_stride, deposition=deposition, x_launch=pos, s0=s0,
-                integrator=integrator, s_max=s_max)
+                integrator=integrator, s_max=s_max, absorption=absorption)
     if (res.status == MAX_STEPS).any():
         raise RuntimeError("make_beam: accepted-step capacity exhausted (raise max_steps)")
     dV = plasma.shell_volumes(g)
