@@ -312,7 +312,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
             psi_a = psi_b;
         }
         if constexpr (TRAJ) {
-            if ((r.steps % a.traj_stride) == 0) {
+            if (a.traj_stride > 0 && (r.steps % a.traj_stride) == 0) {
                 const size_t si = (size_t)(r.steps / a.traj_stride - 1);
                 double *T = a.traj + si * 5 * (size_t)a.n + i;
                 T[0] = x[0];
@@ -573,7 +573,8 @@ __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r
                 }
             }
             if constexpr (TRAJ) {
-                if ((r.steps % a.traj_stride) == 0 && r.steps / a.traj_stride <= a.n_save) {
+                if (a.traj_stride > 0 && (r.steps % a.traj_stride) == 0 &&
+                    r.steps / a.traj_stride <= a.n_save) {
                     double *T = a.traj + (size_t)(r.steps / a.traj_stride - 1) * 5 * a.n + i;
                     T[0] = u[0];
                     T[(size_t)a.n] = u[1];
@@ -1893,16 +1894,19 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     // default: the queue pays off once the beam exceeds one wave per SIMD
     // (measured: 42k rays 111 vs 106 ms one-shot; 100k rays 151 vs 174 ms)
     const bool adaptive = cfg->integrator == 1;
-    const int use_sched = adaptive ? 1  // the adaptive path runs one tspan chunk per visit
+    const int use_sched = adaptive || cfg->absorption >= 2
+                              ? 1  // the adaptive path runs one tspan chunk per visit; warm always queues
                                    : p->sched_mode >= 0 ? p->sched_mode
                                                         : (sched_env && G > p->n_cu * 4 ? 1 : 0);
 // every <absorption, deposition mode, trajectory> instance of a trace kernel
-#define TORJ_DISPATCH_T(L, A, D) \
-    do {                         \
-        if (tr)                  \
-            L(A, D, true);       \
-        else                     \
-            L(A, D, false);      \
+// (warm models: the TRAJ instance only, with traj_stride = 0 when no
+// trajectory is wanted -- fewer instances of the heavy warm code)
+#define TORJ_DISPATCH_T(L, A, D)            \
+    do {                                    \
+        if (tr)                             \
+            L(A, D, true);                  \
+        else                                \
+            L(A, D, ((A) >= 2 ? true : false)); \
     } while (0)
 #define TORJ_DISPATCH_D(L, A)                                 \
     do {                                                      \
@@ -1915,9 +1919,19 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     } while (0)
 #define TORJ_DISPATCH_TRACE(L)              \
     do {                                    \
-        if (cfg->absorption >= 2)           \
+        if (cfg->absorption == 3)           \
+            TORJ_DISPATCH_D(L, 3);          \
+        else if (cfg->absorption == 2)      \
             TORJ_DISPATCH_D(L, 2);          \
         else if (cfg->absorption == 1)      \
+            TORJ_DISPATCH_D(L, 1);          \
+        else                                \
+            TORJ_DISPATCH_D(L, 0);          \
+    } while (0)
+// the one-lane-per-ray kernel: cold and Albajar only (warm always queues)
+#define TORJ_DISPATCH_TRACE01(L)            \
+    do {                                    \
+        if (cfg->absorption == 1)           \
             TORJ_DISPATCH_D(L, 1);          \
         else                                \
             TORJ_DISPATCH_D(L, 0);          \
@@ -1970,7 +1984,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         p->last_sched = false;
         const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
 #define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
-        TORJ_DISPATCH_TRACE(LAUNCH);
+        TORJ_DISPATCH_TRACE01(LAUNCH);
 #undef LAUNCH
     }
     HIPCK(hipGetLastError());
@@ -1978,7 +1992,9 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     if (fit) {
         if (adaptive)
             ;  // the last accepted step's FSAL stage already gave P alpha there
-        else if (cfg->absorption >= 2)
+        else if (cfg->absorption == 3)
+            hipLaunchKernelGGL(k_final_alpha<3>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
+        else if (cfg->absorption == 2)
             hipLaunchKernelGGL(k_final_alpha<2>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         else if (cfg->absorption == 1)
             hipLaunchKernelGGL(k_final_alpha<1>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);

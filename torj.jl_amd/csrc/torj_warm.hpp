@@ -142,6 +142,20 @@ TORJ_HD void ssbi(double zz, int n, int l, double out[kWarmMaxL + 3]) {
     }
 }
 
+// 1/x for normal x > 0: v_rcp_f64 plus two Newton steps on the device
+// (~5 instructions against ~10 for the IEEE division sequence)
+TORJ_HD double rcp_pos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double r = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
 // Faddeeva w(z) for Z(z) = i sqrt(pi) w(z) (zetac, :345-465): Poppe & Wijers,
 // ACM TOMS 680 (series near the origin, Laplace continued fraction / truncated
 // Taylor expansion otherwise, reflection for Im z < 0)
@@ -185,18 +199,19 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
             nu = (int)rint(16.0 + 26.0 * qrho);
         }
         double qlambda = h > 0.0 ? pow(h2, (double)kapn) : 0.0;
+        const double inv_h2 = h > 0.0 ? 1.0 / h2 : 0.0;
         double rx = 0.0, ry = 0.0, sx = 0.0, sy = 0.0;
         for (int n = nu; n >= 0; n--) {
             const double np1 = n + 1.0;
             double tx = yabs + h + np1 * rx, ty = xabs - np1 * ry;
-            const double c = 0.5 / (tx * tx + ty * ty);
+            const double c = 0.5 * rcp_pos(tx * tx + ty * ty);
             rx = c * tx;
             ry = c * ty;
             if (h > 0.0 && n <= kapn) {
                 tx = qlambda + sx;
                 sx = rx * tx - ry * sy;
                 sy = ry * tx + rx * sy;
-                qlambda /= h2;
+                qlambda *= inv_h2;
             }
         }
         if (h == 0.0) {
@@ -230,13 +245,15 @@ TORJ_HD cplx zetac(double x, double y) {
     return {-kSqrtPi * w.im, kSqrtPi * w.re};
 }
 
-struct Tensor {  // epsl(3,3,lrm) upper triangle (11 12 22 13 23 33) + e330
-    cplx e[kWarmMaxL][6];
+template <int L>
+struct Tensor {  // epsl(3,3,lrm) upper triangle (11 12 22 13 23 33) + e330, lrm <= L
+    cplx e[L][6];
     cplx e330;
 };
 
 // the l-sum of the tensor (shared by both models): fl, ca -> epsl(:,:,l)
-TORJ_HD void tensor_store(Tensor &T, int l, double xg, double fl, const cplx ca[6]) {
+template <int L>
+TORJ_HD void tensor_store(Tensor<L> &T, int l, double xg, double fl, const cplx ca[6]) {
     T.e[l - 1][0] = -xg * ca[0] * fl;
     T.e[l - 1][1] = I_times(xg * ca[1] * fl);
     T.e[l - 1][2] = -xg * ca[2] * fl;
@@ -245,13 +262,15 @@ TORJ_HD void tensor_store(Tensor &T, int l, double xg, double fl, const cplx ca[
     T.e[l - 1][5] = -xg * ca[5] * fl;
 }
 
-// weakly relativistic tensor (fsup + dieltens_maxw_wr, :473-638)
-TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor &T) {
-    cplx cefp[kWarmMaxL + 1][3], cefm[kWarmMaxL + 1][3];
-    for (int a = 0; a <= lrm; a++)
-        for (int b = 0; b < 3; b++) cefp[a][b] = cefm[a][b] = C(0.0);
+// Shkarofsky coefficients of one |s| (fsup, :473-561): p[ir] = cefp(isa, ir),
+// m[ir] = cefm(isa, ir), ir = 0..2, summed over is = -isa then +isa in the
+// reference's order.  Only the last three steps of the l-recurrence are
+// stored, so p / m are indexed statically and stay in registers.
+TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
     const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
-    for (int is = -lrm; is <= lrm; is++) {
+    for (int ir = 0; ir < 3; ir++) p[ir] = m[ir] = C(0.0);
+    for (int sg = (isa == 0 ? 1 : -1); sg <= 1; sg += 2) {
+        const int is = sg * isa;
         const double alpha = anpl2hm1 + is * yg, phi2 = amu * alpha, phim = sqrt(fabs(phi2));
         double xp, yp, xm, ym, x0, y0;
         if (alpha >= 0) {
@@ -273,49 +292,74 @@ TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm,
             cf32 = 2.0 * (1.0 - cphi * zetac(x0, y0));
         }
         cplx cf0 = cf12, cf1 = cf32;
-        if (is == 0) cefp[0][0] = cefm[0][0] = cf32;
-        const int isa = abs(is);
-        for (int l = 1; l <= isa + 2; l++) {
+        auto step = [&](int l) {
             const cplx cf2 = apsi > 0.7 ? (1.0 + phi2 * cf0 - (l - 0.5) * cf1) / (psi * psi)
                                          : (1.0 + phi2 * cf1) / (l + 0.5);
-            const int ir = l - isa;
-            if (ir >= 0) {
-                cefp[isa][ir] = cefp[isa][ir] + cf2;
-                cefm[isa][ir] = is > 0 ? cefm[isa][ir] + cf2 : cefm[isa][ir] - cf2;
-            }
             cf0 = cf1;
             cf1 = cf2;
+            return cf2;
+        };
+        if (is == 0) p[0] = m[0] = cf32;
+        for (int l = 1; l < isa; l++) step(l);  // l < isa: not stored
+#pragma unroll
+        for (int ir = 0; ir < 3; ir++) {
+            if (isa + ir < 1) continue;  // s = 0: ir = 0 is cf32 itself
+            const cplx cf2 = step(isa + ir);
+            p[ir] = p[ir] + cf2;
+            m[ir] = is > 0 ? m[ir] + cf2 : m[ir] - cf2;
         }
     }
+}
+
+// weakly relativistic tensor (fsup + dieltens_maxw_wr, :473-638).  The |s|
+// loop runs outermost and adds its terms to every l >= |s|, in the
+// reference's summation order; ca[l][.] is indexed statically (registers).
+template <int L>
+TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor<L> &T) {
     const double anpl2 = anpl * anpl;
-    for (int l = 1; l <= lrm; l++) {
+    cplx ca[L][6];
+#pragma unroll
+    for (int l = 0; l < L; l++)
+        for (int q = 0; q < 6; q++) ca[l][q] = C(0.0);
+    cplx p0[3];
+    for (int isa = 0; isa <= lrm; isa++) {
+        cplx p[3], m[3];
+        fsup_s(yg, anpl, amu, isa, p, m);
+        if (isa == 0) p0[0] = p[0], p0[1] = p[1], p0[2] = p[2];
+        const double is = isa;
+        const cplx cq0p = amu * p[0], cq0m = amu * m[0];
+        const cplx cq1p = amu * anpl * (p[0] - p[1]);
+        const cplx cq1m = amu * anpl * (m[0] - m[1]);
+        const cplx cq2p = p[1] + amu * anpl2 * (p[2] + p[0] - 2.0 * p[1]);
+#pragma unroll
+        for (int l = 1; l <= L; l++) {
+            if (l > lrm || l < isa) continue;
+            const int lm = l - 1, k = l - isa;
+            const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(isa + l) * factd(l - isa));
+            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + isa)) / (2 * l - 1));
+            ca[lm][0] = ca[lm][0] + (is * is) * asl * cq0p;
+            ca[lm][1] = ca[lm][1] + (is * l) * asl * cq0m;
+            ca[lm][2] = ca[lm][2] + bsl * cq0p;
+            ca[lm][3] = ca[lm][3] + is * asl * cq1m / yg;
+            ca[lm][4] = ca[lm][4] + (double)l * asl * cq1p / yg;
+            ca[lm][5] = ca[lm][5] + asl * cq2p / (yg * yg);
+        }
+    }
+#pragma unroll
+    for (int l = 1; l <= L; l++) {
+        if (l > lrm) break;
         const int lm = l - 1;
         const double fcl = pow(0.5, l) * pow((1.0 / yg) * (1.0 / yg) / amu, lm) * factd(2 * l) / factd(l);
-        cplx ca[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
-        for (int is = 0; is <= l; is++) {
-            const int k = l - is;
-            const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(is + l) * factd(l - is));
-            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + is)) / (2 * l - 1));
-            const cplx cq0p = amu * cefp[is][0], cq0m = amu * cefm[is][0];
-            const cplx cq1p = amu * anpl * (cefp[is][0] - cefp[is][1]);
-            const cplx cq1m = amu * anpl * (cefm[is][0] - cefm[is][1]);
-            const cplx cq2p = cefp[is][1] + amu * anpl2 * (cefp[is][2] + cefp[is][0] - 2.0 * cefp[is][1]);
-            ca[0] = ca[0] + (double)(is * is) * asl * cq0p;
-            ca[1] = ca[1] + (double)(is * l) * asl * cq0m;
-            ca[2] = ca[2] + bsl * cq0p;
-            ca[3] = ca[3] + (double)is * asl * cq1m / yg;
-            ca[4] = ca[4] + (double)l * asl * cq1p / yg;
-            ca[5] = ca[5] + asl * cq2p / (yg * yg);
-        }
-        tensor_store(T, l, xg, fcl, ca);
+        tensor_store(T, l, xg, fcl, ca[lm]);
     }
-    const cplx cq2p = cefp[0][1] + amu * anpl2 * (cefp[0][2] + cefp[0][0] - 2.0 * cefp[0][1]);
+    const cplx cq2p = p0[1] + amu * anpl2 * (p0[2] + p0[0] - 2.0 * p0[1]);
     T.e330 = 1.0 - xg * amu * cq2p;
 }
 
 // fully relativistic tensor (hermitian iwarm > 2 + antihermitian +
 // dieltens_maxw_fr, :646-1134)
-TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm, Tensor &T) {
+template <int L>
+TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm, Tensor<L> &T) {
     const int llm = lrm < 3 ? lrm : 3;
     // rr[n + 3][k][m], n in [-llm, llm], m in [|n|, llm]
     double rr[7][3][4];
@@ -413,10 +457,13 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
     auto RR = [&](int n, int k, int m) -> double {
         return (n >= -3 && n <= 3 && m <= 3) ? rr[n + 3][k][m] : 0.0;
     };
-    for (int l = 1; l <= lrm; l++) {
+#pragma unroll
+    for (int l = 1; l <= L; l++) {  // static l, is: the tensor stays in registers
+        if (l > lrm) break;
         const int lm = l - 1;
         const double fal = -pow(0.25, l) * factd(2 * l) / (factd(l) * factd(l) * pow(yg, 2 * lm));
         cplx ca[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
+#pragma unroll
         for (int is = 0; is <= l; is++) {
             const int k = l - is;
             const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(is + l) * factd(l - is));
@@ -446,15 +493,18 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
 }
 
 // warmdisp (:1158-1267) -> N_perp^2 (complex); anpr2 initialised (R2)
+template <int L>
 TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int sox, int lrm,
-                          const Tensor &T) {
+                          const Tensor<L> &T) {
     cplx anpr2a = C(anprc * anprc), anpr2 = anpr2a;
     const double anpl2 = anpl * anpl;
     double errnpr = 1.0;
     for (int i = 1; i <= 100; i++) {
         cplx s[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
         cplx pw = C(1.0);
-        for (int l = 0; l < lrm; l++) {
+#pragma unroll
+        for (int l = 0; l < L; l++) {  // static l: the tensor stays in registers
+            if (l >= lrm) break;
             for (int q = 0; q < 6; q++) s[q] = s[q] + T.e[l][q] * pw;
             pw = pw * anpr2a;
         }
@@ -515,29 +565,52 @@ TORJ_HD int larmornumber(double yg, double npl, double mu) {
 #ifndef TORJ_WARM_ATTR
 #define TORJ_WARM_ATTR TORJ_HD
 #endif
-TORJ_WARM_ATTR double alpha_warm(double omega, double X, double Y, double N_abs, double N_par,
-                                 double Te, double inv_dDdN, int mode, int iwarm, cplx *n2) {
-    const double mu = kMe * kC * kC / (Te * kE);
-    const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
-    const int nharm = larmornumber(Y, N_par, mu);
-    const int lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
-    Tensor T;
-    if (iwarm == 1)
-        dieltens_wr(X, Y, N_par, mu, lrm, T);
+template <int IWARM, int L>
+TORJ_HD double alpha_core(double omega, double X, double Y, double N_par, double mu, double npr,
+                          int lrm, double inv_dDdN, int mode, cplx *n2) {
+    Tensor<L> T;
+    if constexpr (IWARM == 1)
+        dieltens_wr<L>(X, Y, N_par, mu, lrm, T);
     else
-        dieltens_fr(X, Y, N_par, mu, lrm, T);
+        dieltens_fr<L>(X, Y, N_par, mu, lrm, T);
     // identity on the l = 1 diagonal (:629-630 / :1125-1126)
     T.e[0][0] = T.e[0][0] + 1.0;
     T.e[0][2] = T.e[0][2] + 1.0;
     const int sox = Y <= 1.0 ? mode : -mode;
-    const cplx a2 = warmdisp_n2(X, Y, N_par, npr, sox, lrm, T);
+    const cplx a2 = warmdisp_n2<L>(X, Y, N_par, npr, sox, lrm, T);
     if (n2) *n2 = a2;
     return 2.0 * a2.im * omega / kC * inv_dDdN;
 }
 
-// one RHS evaluation: ABS 0 cold, 1 Albajar (abs_Albajar_fast), 2 warm with
-// iwarm = 1 (model 2, weakly relativistic) or 3 (model 3, fully relativistic);
-// separate instances keep the warm module's private frame out of the others
+// The tensor is sized for lrm <= 3 (the common case: one to three Larmor
+// orders up to the third harmonic) or lrm <= 5; on the device the choice is
+// made per wave (ballot), so the heavy code never diverges between the two.
+template <int IWARM>
+TORJ_WARM_ATTR double alpha_warm_t(double omega, double X, double Y, double N_abs, double N_par,
+                                   double Te, double inv_dDdN, int mode, cplx *n2) {
+    const double mu = kMe * kC * kC / (Te * kE);
+    const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
+    const int nharm = larmornumber(Y, N_par, mu);
+    const int lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
+#if defined(__HIP_DEVICE_COMPILE__)
+    const bool big = __ballot(lrm > 3) != 0;
+#else
+    const bool big = lrm > 3;
+#endif
+    return big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode, n2)
+               : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode, n2);
+}
+
+// runtime iwarm (1 or 3): the point entry torj_alpha_warm and the host tests
+TORJ_HD double alpha_warm(double omega, double X, double Y, double N_abs, double N_par, double Te,
+                          double inv_dDdN, int mode, int iwarm, cplx *n2) {
+    return iwarm == 1 ? alpha_warm_t<1>(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode, n2)
+                      : alpha_warm_t<3>(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode, n2);
+}
+
+// one RHS evaluation: ABS 0 cold, 1 Albajar (abs_Albajar_fast), 2 warm weakly
+// relativistic (iwarm 1), 3 warm fully relativistic (iwarm 3); separate
+// instances keep each model's registers and private frame out of the others
 template <int ABS>
 TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Consts &k,
                        const GLTable &gl, double omega, int mode, int model, const double x[3],
@@ -549,10 +622,10 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
     if constexpr (ABS == 1) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
-    } else if constexpr (ABS == 2) {
+    } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = alpha_warm(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode, model == 2 ? 1 : 3,
-                           nullptr);
+        alpha = alpha_warm_t<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode,
+                                               nullptr);
     } else {
         alpha = 0.0;
     }
