@@ -343,3 +343,42 @@ def test_make_beam_self_consistency(gpu, T, eq):
     P_test = np.sum(dVdpsi * dP_dV * (grid[1] - grid[0]))
     assert abs(pabs - P_test) <= 1e-3 + 1e-3 * pabs
     assert pabs > 0.5  # the X2 resonance is crossed
+
+
+def test_c2_full_fan_o_mode(gpu, T, hplasma, oplasma, fan_states):
+    """BASELINE configs[1] / SURVEY C2: the 14-ring fan truncated to 1 024 rays,
+    O-mode, 92.5 GHz, 2 000 RK4 steps of 1e-4 m, GPU vs oracle <= 1e-10."""
+    xp, Np, w, om = fan_states[-1]
+    assert len(w) >= 1024
+    xp, Np, w = xp[:1024], Np[:1024], w[:1024]
+    grid = np.linspace(0, 1, 1000)
+    g = T.trace(hplasma, xp, Np, om, -1, ds=1e-4, n_steps=2000, psi_grid=grid, weights=w)
+    o = oplasma.trace(xp, Np, om, -1, 1e-4, 2000, psi_grid=grid, weights=w)
+    _compare_trace(g, o)
+    assert np.abs(g.dP_shell[:-1] - o["dP"]).max() <= 1e-10 * max(np.abs(o["dP"]).max(), 1e-300)
+
+
+def test_trace_on_129_grid(gpu, T, O):
+    """the 129 x 129 equilibrium variant (coefficients 1.1 MB, past
+    LDS, L2-resident): fields and 2 000-step traces vs the oracle."""
+    from torj_hip import synthetic as S
+
+    eq = S.circular_tokamak(nR=129, nZ=129)
+    hp = T.Plasma(*S.plasma_args(eq))
+    op = O.OraclePlasma(*S.plasma_args(eq))
+    rng = np.random.default_rng(5)
+    x = np.stack([rng.uniform(1.3, 2.1, 64), rng.uniform(-0.3, 0.3, 64), rng.uniform(-0.3, 0.3, 64)], 1)
+    Bh = T.B_spline(hp, x)
+    Bo = np.array([op.B_spline(p) for p in x])
+    assert np.abs(Bh - Bo).max() <= 1e-12 * np.abs(Bo).max()
+    s = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], s["f_abs_test"],
+                                            N_rings=4, min_azimuthal_points=5)
+    om = 2 * np.pi * s["f_abs_test"]
+    xp, Np, s0, st = T.ray_entry(hp, pos, dirs, om, 1)
+    assert (st == 0).all()
+    g = T.trace(hp, xp, Np, om, 1, ds=1e-4, n_steps=2000)
+    o = op.trace(xp, Np, om, 1, 1e-4, 2000)
+    _compare_trace(g, o)

@@ -690,8 +690,13 @@ __device__ __forceinline__ void sched_publish_begin() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// warm kernels: one wave per SIMD -- the 512-VGPR budget holds the warm
+// tensor without spills (C5: 458 vs 505 ms at two waves per SIMD)
+#ifndef TORJ_WARM_MIN_WAVES
+#define TORJ_WARM_MIN_WAVES 1
+#endif
 template <int ABS, int DEPO, bool TRAJ, int INTEG>
-__global__ void __launch_bounds__(64, TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
+__global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_WAVES) k_trace_sched(TraceArgs a, SchedCtl *ctl,
                                                                      unsigned long long *slots,
                                                                      unsigned S, int G, int cs) {
     extern __shared__ double lds_k[];  // integrator 1: Tsit5 stage vectors of this wave
@@ -1959,7 +1964,9 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         }();
         int W = p->sched_waves > 0 ? p->sched_waves
                 : w_env > 0        ? w_env
-                                   : std::min(p->n_cu * 4 * 2, G - G / 16);
+                                   : std::min(p->n_cu * 4 * (cfg->absorption >= 2 ? TORJ_WARM_MIN_WAVES
+                                                                                  : TORJ_MIN_WAVES),
+                                              G - G / 16);
         W = std::max(1, std::min(W, G));
         const unsigned S = 4u * (unsigned)(G + W);  // ring slots (tag check makes reuse safe)
         const size_t bytes = 256 + (size_t)S * sizeof(unsigned long long);

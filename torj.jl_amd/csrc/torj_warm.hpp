@@ -25,14 +25,17 @@ TORJ_HD cplx operator-(cplx a) { return {-a.re, -a.im}; }
 TORJ_HD cplx operator*(cplx a, cplx b) { return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re}; }
 TORJ_HD cplx operator*(double s, cplx a) { return {s * a.re, s * a.im}; }
 TORJ_HD cplx operator*(cplx a, double s) { return {s * a.re, s * a.im}; }
-TORJ_HD cplx operator/(cplx a, double s) { return {a.re / s, a.im / s}; }
+TORJ_HD cplx operator/(cplx a, double s) {
+    const double r = 1.0 / s;
+    return {a.re * r, a.im * r};
+}
 TORJ_HD cplx operator/(cplx a, cplx b) {  // Smith's algorithm
     if (fabs(b.re) >= fabs(b.im)) {
-        const double r = b.im / b.re, d = b.re + b.im * r;
-        return {(a.re + a.im * r) / d, (a.im - a.re * r) / d};
+        const double r = b.im / b.re, id = 1.0 / (b.re + b.im * r);
+        return {(a.re + a.im * r) * id, (a.im - a.re * r) * id};
     }
-    const double r = b.re / b.im, d = b.re * r + b.im;
-    return {(a.re * r + a.im) / d, (a.im * r - a.re) / d};
+    const double r = b.re / b.im, id = 1.0 / (b.re * r + b.im);
+    return {(a.re * r + a.im) * id, (a.im * r - a.re) * id};
 }
 TORJ_HD cplx operator+(double s, cplx a) { return {s + a.re, a.im}; }
 TORJ_HD cplx operator-(double s, cplx a) { return {s - a.re, -a.im}; }
@@ -162,7 +165,7 @@ TORJ_HD double rcp_pos(double x) {
 TORJ_HD cplx faddeeva(double xi, double yi) {
     const double factor = 1.12837916709551257388;  // 2/sqrt(pi)
     const double xabs = fabs(xi), yabs = fabs(yi);
-    const double x = xabs / 6.3, y = yabs / 4.4;
+    const double x = xabs * (1.0 / 6.3), y = yabs * (1.0 / 4.4);
     double qrho = x * x + y * y;
     const double xquad = xabs * xabs - yabs * yabs, yquad = 2.0 * xabs * yabs;
     double u, v, u2 = 0.0, v2 = 0.0;
@@ -174,9 +177,10 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
         double xsum = 1.0 / j, ysum = 0.0;
         for (int i = n; i >= 1; i--) {
             j -= 2;
-            const double xaux = (xsum * xquad - ysum * yquad) / i;
-            ysum = (xsum * yquad + ysum * xquad) / i;
-            xsum = xaux + 1.0 / j;
+            const double ri = rcp_pos((double)i);
+            const double xaux = (xsum * xquad - ysum * yquad) * ri;
+            ysum = (xsum * yquad + ysum * xquad) * ri;
+            xsum = xaux + rcp_pos((double)j);
         }
         const double u1 = -factor * (xsum * yabs + ysum * xabs) + 1.0;
         const double v1 = factor * (xsum * xabs - ysum * yabs);
@@ -268,6 +272,8 @@ TORJ_HD void tensor_store(Tensor<L> &T, int l, double xg, double fl, const cplx 
 // stored, so p / m are indexed statically and stay in registers.
 TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
     const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
+    const bool big_psi = apsi > 0.7;
+    const double ipsi2 = big_psi ? 1.0 / (psi * psi) : 0.0, i2psi = big_psi ? 0.5 / psi : 0.0;
     for (int ir = 0; ir < 3; ir++) p[ir] = m[ir] = C(0.0);
     for (int sg = (isa == 0 ? 1 : -1); sg <= 1; sg += 2) {
         const int is = sg * isa;
@@ -278,23 +284,44 @@ TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx
         } else {
             xp = psi, yp = phim, xm = -psi, ym = phim, x0 = 0.0, y0 = phim;
         }
-        const cplx czp = zetac(xp, yp), czm = zetac(xm, ym);
+        // one zetac call site for the two (three) arguments: a single inlined copy
+        // of the Faddeeva code per tensor instance.  Below the resonance
+        // (alpha < 0) z_m = -conj(z_p), and the algorithm's w(-conj z) is
+        // conj(w(z)) bit for bit (it evaluates |x| and flips Im w), so Z(z_m) =
+        // -conj(Z(z_p)) and one evaluation serves both.
+        cplx czp, czm, cz0;
+        const bool mirror = alpha < 0;
+        const int nz = big_psi ? 2 : 3;
+#pragma unroll 1
+        for (int kz = 0; kz < nz; kz++) {
+            if (kz == 1 && mirror) continue;
+            const double zx = kz == 0 ? xp : (kz == 1 ? xm : x0);
+            const double zy = kz == 0 ? yp : (kz == 1 ? ym : y0);
+            const cplx z = zetac(zx, zy);
+            if (kz == 0)
+                czp = z;
+            else if (kz == 1)
+                czm = z;
+            else
+                cz0 = z;
+        }
+        if (mirror) czm = C(-czp.re, czp.im);
         cplx cf12 = C(0.0);
-        if (alpha > 0)
-            cf12 = -(czp + czm) / (2.0 * phim);
-        else if (alpha < 0)
-            cf12 = -I_times((czp + czm) / (2.0 * phim));
+        if (alpha != 0.0) {
+            const double i2phim = 0.5 * rcp_pos(phim);
+            cf12 = alpha > 0 ? -((czp + czm) * i2phim) : -I_times((czp + czm) * i2phim);
+        }
         cplx cf32;
-        if (apsi > 0.7) {
-            cf32 = -(czp - czm) / (2.0 * psi);
+        if (big_psi) {
+            cf32 = -((czp - czm) * i2psi);
         } else {
             const cplx cphi = alpha < 0 ? C(0.0, -phim) : C(phim);
-            cf32 = 2.0 * (1.0 - cphi * zetac(x0, y0));
+            cf32 = 2.0 * (1.0 - cphi * cz0);
         }
         cplx cf0 = cf12, cf1 = cf32;
         auto step = [&](int l) {
-            const cplx cf2 = apsi > 0.7 ? (1.0 + phi2 * cf0 - (l - 0.5) * cf1) / (psi * psi)
-                                         : (1.0 + phi2 * cf1) / (l + 0.5);
+            const cplx cf2 = big_psi ? (1.0 + phi2 * cf0 - (l - 0.5) * cf1) * ipsi2
+                                     : (1.0 + phi2 * cf1) * rcp_pos(l + 0.5);
             cf0 = cf1;
             cf1 = cf2;
             return cf2;
