@@ -158,4 +158,19 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     return arc_lengths, trajectories, ray_powers, dP_dV, dP[end], w
 end
 
+"""alpha(...) of src/general_absorption.jl:1328-1337 (repaired, DESIGN.md §3.6) at n
+points on the GPU: iwarm 1 (weakly) or 3 (fully relativistic); inv_dDdN = 1/|dD/dN|.
+Returns (alpha, N_perp^2)."""
+function alpha_warm(omega::Vector{Float64}, X::Vector{Float64}, Y::Vector{Float64},
+                    N_abs::Vector{Float64}, N_par::Vector{Float64}, Te::Vector{Float64},
+                    inv_dDdN::Vector{Float64}, mode::Integer, iwarm::Integer)
+    n = length(X)
+    alpha, n2 = zeros(n), zeros(2n)
+    check(ccall((:torj_alpha_warm, libtorj), Cint,
+                (Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Cint, Cint, Ptr{Float64}, Ptr{Float64}),
+                n, omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode, iwarm, alpha, n2))
+    return alpha, complex.(n2[1:2:end], n2[2:2:end])
+end
+
 end # module
