@@ -139,6 +139,10 @@ def main():
             d_status.data_ptr(), d_steps.data_ptr(), d_dP.data_ptr(), d_Pdep.data_ptr(),
             d_traj.data_ptr() if n_save else None, counters, stream.cuda_stream))
 
+    def progress(msg):  # heartbeat on stderr (long warm-model launches), never on stdout
+        if rank == 0:
+            print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
     def one_step(ev=None):
         if ev is not None:
             ev[0].record(stream)
@@ -152,10 +156,13 @@ def main():
     d_cnt.zero_()
     launch(d_cnt.data_ptr())
     T._lib.check(L.torj_trace_check(plasma.handle, stream.cuda_stream))  # all groups retired
+    progress("counted launch done")
     cnt = d_cnt.cpu().numpy().astype(np.int64)
     ray_steps_local = int(cnt[0])
-    for _ in range(args.warmup):
+    for k in range(args.warmup):
         one_step()
+        torch.cuda.synchronize(dev)
+        progress(f"warmup {k + 1}/{args.warmup} done")
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -172,6 +179,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     T._lib.check(L.torj_trace_check(plasma.handle, stream.cuda_stream))
+    progress(f"timed region done: {elapsed:.2f} s")
     hot_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))  # whole torj_trace_device_ex call
     import ctypes
     n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
@@ -261,6 +269,7 @@ def main():
         if world == 1:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,
                                             pos, s0)
+            progress("host-pointer call done")
             out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
