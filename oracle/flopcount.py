@@ -187,31 +187,36 @@ def series_terms(x_m):
     return 9 if x_m <= 1.0 else 12 if x_m <= 2.0 else 14 if x_m <= 3.0 else 16 if x_m <= 4.0 else 44
 
 
-def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, sqNp, Nperp, omega_bar, Axz, ea, e3, m,
-                     count=None):
-    """Node-pair form of abs_Al_integral_nume_fast x sqrt((m/m0)^2-1) (torj_math.hpp)."""
+def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m, count=None):
+    """Node-pair form of abs_Al_integral_nume_fast x sqrt((m/m0)^2-1) (torj_math.hpp
+    albajar_harmonic + pair_term, TORJ_PAIR_V2): the pair (+t, -t) shares every
+    t-even factor, bracket(+-t) = P +- t Q, gamma(+-t)^2 = C0 + C1 t^2 +- C2 t."""
     md = float(m)
+    inv_md = 1.0 / md  # compile-time constant
     r2m1 = r * r - 1.0
     sq_r = sqrt(r2m1)
     x_m = Nperp * omega_bar * sq_r
-    q = x_m / (md * sqNp)
+    q = x_m * inv_sqNp * inv_md
     K0 = Axz * Axz + ea * ea
-    K1 = Axz * ea * x_m / md
-    K2 = 4.0 * ea * ea / (md * md)
+    K1 = Axz * ea * x_m * inv_md
+    K2 = 4.0 * ea * ea * (inv_md * inv_md)
     K3 = q * q * e3 * e3
     K4 = 2.0 * q * Axz * e3
-    K5 = q * ea * e3 * x_m / md
+    K5 = q * ea * e3 * x_m * inv_md
     upa0, upa1 = inv_sqNp * r * Npar, inv_sqNp * sq_r
+    C0 = upa0 * upa0 + r * r
+    C1 = r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp)
+    C2 = 2.0 * upa0 * upa1
+    hx = 0.5 * x_m
     K = series_terms(x_m.v)
     if count is not None:
         count["harm_setup"] = Counter.n - count["_t0"]
     total = CF(0)
     n = len(gl)
     for i in range(n // 2 + (n & 1)):
-        t, w, st = gl[i]
+        t, w, st, t2 = gl[i]
         single = (n & 1) and i == n // 2
-        arg = x_m * st
-        h = 0.5 * arg
+        h = hx * st
         h2 = h * h
         z = -h2
         n0 = Counter.n
@@ -224,19 +229,30 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, sqNp, Nperp, omega_bar, Axz, ea,
         p = h
         for _ in range(1, 2 * m - 1):
             p = p * h
-        A = h * (Sm * Sm)
-        B = h * (K2 * h2 * Sl * Sm1)
-        Cc = st * Sm * (Sl - h2 * Sm1)
+        hSm = h * Sm
+        A = hSm * Sm
+        T1 = h2 * Sm1
+        B = K2 * Sl * (h * T1)
+        Cc = st * Sm * (Sl - T1)
+        P = A * (K3 * t2 + K0) + (Cc * K1 - B)
         wp = w * p
-        u_perp1 = 1.0 + r2m1 * (1.0 - t * t)
-        n1 = Counter.n
-        for tt in ((t,) if single else (t, -t)):
-            br = A * (tt * (K3 * tt + K4) + K0) - B + Cc * (K5 * tt + K1)
-            up = upa1 * tt + upa0
-            g = sqrt(up * up + u_perp1)
-            total = total + (wp * br) * exp(mu * (1.0 - g))
-            if count is not None and "node" not in count:
-                count["node"] = Counter.n - n1
+        a = C1 * t2 + C0
+        n_node = 0
+        if single:
+            n1 = Counter.n
+            E = exp(mu - mu * sqrt(a))
+            n_node = Counter.n - n1
+            total = total + wp * P * E
+        else:
+            Q = A * K4 + Cc * K5
+            b = C2 * t
+            n1 = Counter.n
+            Ep = exp(mu - mu * sqrt(a + b))
+            n_node = Counter.n - n1
+            Em = exp(mu - mu * sqrt(a - b))
+            total = total + wp * (P * (Ep + Em) + (t * Q) * (Ep - Em))
+        if count is not None and "node" not in count:
+            count["node"] = n_node
         if count is not None and "pair_shared" not in count:
             count["pair_shared"] = (Counter.n - n0) - n_series - (2 - bool(single)) * count["node"]
             count["term"] = n_series / (K - 1)
@@ -249,48 +265,58 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, sqNp, Nperp, omega_bar, Axz, ea,
 
 
 def abs_albajar_fast(gl, omega, X, Y, Nabs, Npar, Te, mode, count=None):
+    """torj_math.hpp abs_albajar_fast (src/absorption.jl:191-226 restated for the
+    device: sqrt(1 - cos^2) for sin(acos(cos)), one reciprocal per denominator)."""
     if count is not None:
         count["_t0"] = Counter.n
     if Te < 20.0:
         return CF(0)
-    mu = ME * C_LIGHT * C_LIGHT / (E * Te)
+    kmu = ME * C_LIGHT * C_LIGHT / E  # compile-time constant
+    inv_mu = Te * (1.0 / kmu)
+    mu = kmu * (1.0 / Te)
     omega_bar = 1.0 / Y
-    cos_t = Npar / Nabs
-    sin_t = sin(acos(cos_t))
+    cos_t = Npar * (1.0 / Nabs)
+    sin_t = sqrt(1.0 - cos_t * cos_t)
     Nperp = sqrt(Nabs * Nabs - Npar * Npar)
     if X >= 1.0:
         return CF(0)
     s2, c2, omX = sin_t * sin_t, cos_t * cos_t, 1.0 - X
-    rho = sqrt(Y * Y * (s2 * s2) + 4.0 * omX * omX * c2)
-    f = (2.0 * omX) / (2.0 * omX - Y * Y * s2 - float(mode) * Y * rho)
+    Y2, invY2 = Y * Y, omega_bar * omega_bar
+    rho = sqrt(Y2 * (s2 * s2) + 4.0 * omX * omX * c2)
+    f = (2.0 * omX) * (1.0 / (2.0 * omX - Y2 * s2 - float(mode) * Y * rho))
     Nt = 1.0 - X * f
     if Nt < 0.0:
         return CF(0)
     Nt = sqrt(Nt)
     if not (Nt > 0.0) or Nt > 1.0:
         return CF(0)
-    g = 1.0 - (1.0 - Y * Y) * f
+    inv_Nt = 1.0 / Nt
+    g = 1.0 - (1.0 - Y2) * f
     if c2 < 1e-5 or 1.0 - s2 < 1e-5:
         if mode > 0:
-            ea = sqrt(1.0 / Nt)
-            e1 = -(1.0 / Y * g) * ea
+            ea = sqrt(inv_Nt)
+            e1 = -(omega_bar * g) * ea
             e3 = CF(0)
         else:
-            e1, ea, e3 = CF(0), CF(0), sqrt(1.0 / Nt)
+            e1, ea, e3 = CF(0), CF(0), sqrt(inv_Nt)
     else:
-        den = omX - Nt * Nt * s2
-        ta = 1.0 + ((omX * Nt * Nt * c2) / (den * den)) * 1.0 / (Y * Y) * (g * g)
-        tb = 1.0 + (omX / den) * 1.0 / (Y * Y) * (g * g)
-        ea = sqrt(1.0 / (Nt * sqrt(s2 * (ta * ta) + c2 * (tb * tb))))
+        Nt2 = Nt * Nt
+        den = omX - Nt2 * s2
+        inv_den = 1.0 / den
+        gg = invY2 * (g * g)
+        ta = 1.0 + (omX * Nt2 * c2) * (inv_den * inv_den) * gg
+        tb = 1.0 + (omX * inv_den) * gg
+        ea = sqrt(inv_Nt * (1.0 / sqrt(s2 * (ta * ta) + c2 * (tb * tb))))
         if mode <= 0:
             ea = -ea
-        e1 = -(1.0 / Y * g) * ea
-        e3 = -((Nt * Nt * sin_t * cos_t) / den) * e1
+        e1 = -(omega_bar * g) * ea
+        e3 = -((Nt2 * sin_t * cos_t) * inv_den) * e1
     sqNp = sqrt(1.0 - Npar * Npar)
     m0 = sqNp * omega_bar
     inv_sqNp = 1.0 / sqNp
-    N_eff = (Nperp * Npar) / (1.0 - Npar * Npar)
+    N_eff = (Nperp * Npar) * (inv_sqNp * inv_sqNp)
     Axz = e1 + N_eff * e3
+    inv_m0 = inv_sqNp * Y
     if count is not None:
         count["alpha_pre"] = Counter.n - count["_t0"]
     c_abs = CF(0)
@@ -299,15 +325,15 @@ def abs_albajar_fast(gl, omega, X, Y, Nabs, Npar, Te, mode, count=None):
         if not (m < m0):
             if hc is not None:
                 hc["_t0"] = Counter.n
-            c_abs = c_abs + albajar_harmonic(gl, mu, m / m0, Npar, inv_sqNp, sqNp, Nperp,
+            c_abs = c_abs + albajar_harmonic(gl, mu, m * inv_m0, Npar, inv_sqNp, Nperp,
                                              omega_bar, Axz, ea, e3, m, count=hc)
             hc = None
     n1 = Counter.n
-    a = 1.0 / (1.0 + 105.0 / (128.0 * mu * mu) + 15.0 / (8.0 * mu))
-    sm = sqrt(mu / (2.0 * math.pi))
+    a = 1.0 / (inv_mu * (inv_mu * (105.0 / 128.0) + 15.0 / 8.0) + 1.0)
+    sm = sqrt(mu * (1.0 / (2.0 * math.pi)))
     c_abs = c_abs * (a * (sm * sm * sm))
-    c_abs = -(c_abs * 2.0 * math.pi * math.pi / m0)
-    res = c_abs * X * omega / (Y * C_LIGHT)
+    c_abs = -(c_abs * (2.0 * math.pi * math.pi) * inv_m0)
+    res = c_abs * X * omega * (omega_bar * (1.0 / C_LIGHT))
     if count is not None:
         count["alpha_post"] = Counter.n - n1
     return res
@@ -316,7 +342,7 @@ def abs_albajar_fast(gl, omega, X, Y, Nabs, Npar, Te, mode, count=None):
 def gl_table(n):
     import numpy as np
     t, w = np.polynomial.legendre.leggauss(n)
-    return [(float(a), float(b), math.sqrt(1.0 - a * a)) for a, b in zip(t, w)]
+    return [(float(a), float(b), math.sqrt(1.0 - a * a), float(a * a)) for a, b in zip(t, w)]
 
 
 def measure(coef, g, x, N, omega, mode, n_gl=24):

@@ -4,6 +4,8 @@
 // without a GPU.  Test harness only; the product calls these on the device.
 #include "torj_warm.hpp"
 
+#include <mutex>
+
 extern "C" {
 void wh_zetac(int n, const double *x, const double *y, double *out) {
     for (int i = 0; i < n; i++) {
@@ -32,5 +34,26 @@ void wh_alpha_warm(int n, const double *om, const double *X, const double *Y, co
         alpha[i] = torj::alpha_warm(om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], inv[i], mode, iwarm, &c);
         n2[2 * i] = c.re, n2[2 * i + 1] = c.im;
     }
+}
+
+// abs_Albajar_fast of the product (torj_math.hpp, host build: same arithmetic
+// as the device except that the hardware reciprocal seed and the node-loop
+// sqrt/exp are the exact host ones)
+static torj::GLTable g_wh_gl;
+static std::once_flag g_wh_gl_once;
+void wh_albajar(int n, const double *om, const double *X, const double *Y, const double *Nabs,
+                const double *Npar, const double *Te, int mode, const double *t, const double *w,
+                int ngl, double *alpha) {
+    std::call_once(g_wh_gl_once, [&] {
+        g_wh_gl.n = ngl;
+        for (int i = 0; i < torj::kMaxGL; i++) {  // ascending nodes, zero-padded (torj_abs_al_init)
+            g_wh_gl.t[i] = i < ngl ? t[i] : 0.0;
+            g_wh_gl.w[i] = i < ngl ? w[i] : 0.0;
+            g_wh_gl.st[i] = i < ngl ? sqrt(1.0 - t[i] * t[i]) : 0.0;
+            g_wh_gl.t2[i] = i < ngl ? t[i] * t[i] : 0.0;
+        }
+    });
+    for (int i = 0; i < n; i++)
+        alpha[i] = torj::abs_albajar_fast(g_wh_gl, om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], mode, nullptr);
 }
 }

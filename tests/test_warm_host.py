@@ -107,3 +107,31 @@ def test_alpha_warm_matches_oracle(H, O, mode, iwarm, te_lo, tol_n2, tol_a):
     e_a = np.abs(a - ar) / (np.abs(ar) + floor + 1e-300)
     assert conv.sum() > 0.8 * n
     assert e_n[conv].max() <= tol_n2 and e_a[conv].max() <= tol_a
+
+
+def test_albajar_host_build_matches_golden(H):
+    """abs_Albajar_fast of the product (host build of torj_math.hpp, the same
+    restated prologue the kernels run: rcp_nz quotients, sqrt(1 - cos^2) for
+    sin(acos(cos))) against the oracle's golden sweep: identical NaN / zero
+    pattern (the edge semantics of src/absorption.jl:191-226), 1e-10 relative
+    elsewhere."""
+    import json
+    d = json.load(open(os.path.join(HERE, "golden", "albajar.json")))
+    rows = np.array(d["rows"], dtype=float)
+    H.wh_albajar.argtypes = [C.c_int] + [_dp] * 6 + [C.c_int, _dp, _dp, C.c_int, _dp]
+    t, w = np.polynomial.legendre.leggauss(24)
+    for mode in (-1, 1):
+        r = rows[rows[:, 6] == mode]
+        n = len(r)
+        out = np.zeros(n)
+        cols = [np.ascontiguousarray(r[:, k]) for k in range(6)]
+        H.wh_albajar(n, *[_d(c) for c in cols], mode, _d(t), _d(w), 24, _d(out))
+        want = r[:, 7]
+        nan = np.isnan(want)
+        assert np.array_equal(np.isnan(out), nan)
+        zero = want == 0
+        assert np.all(out[zero] == 0)
+        big = ~nan & ~zero & (np.abs(want) > 1e-12)
+        assert (np.abs(out[big] - want[big]) / np.abs(want[big])).max() < 1e-10
+        small = ~nan & ~zero & ~big
+        assert np.abs(out[small] - want[small]).max() < 1e-20

@@ -1347,7 +1347,10 @@ int torj_abs_al_init(int n) {
     GLTable t{};
     t.n = n;
     gauss_legendre(n, t.t, t.w);
-    for (int i = 0; i < n; i++) t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);
+    for (int i = 0; i < n; i++) {
+        t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);
+        t.t2[i] = t.t[i] * t.t[i];
+    }
     g_gl_host = t;
     g_gl_version++;
     return 0;

@@ -58,6 +58,33 @@ TORJ_HD void bweights(double d, double w[4], double dw[4]) {
 
 TORJ_HD double clampd(double x, double lo, double hi) { return x > hi ? hi : (x < lo ? lo : x); }
 
+// 1/x for the denominators of the ray RHS and the absorption prologue: on the
+// device v_rcp_f64 + two Newton steps (<= 1 ulp) instead of the IEEE division
+// sequence (div_scale x2, rcp, five fma, div_fmas, div_fixup per quotient).
+// Special operands give NaN (0 and inf included), on the host too (same Newton
+// steps after an exact 1/x), so host and device agree on which results are
+// finite; the callers only pass denominators that are finite and non-zero on
+// every physical input (a zero means a resonance/cutoff the reference also
+// turns into a non-finite result).
+#ifndef TORJ_FAST_RCP
+#define TORJ_FAST_RCP 1
+#endif
+TORJ_HD double rcp_nz(double x) {
+#if TORJ_FAST_RCP
+#ifdef __HIP_DEVICE_COMPILE__
+    double r = __builtin_amdgcn_rcp(x);
+#else
+    double r = 1.0 / x;
+#endif
+    double e = fma(-x, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-x, r, 1.0);
+    return fma(r, e, r);
+#else
+    return 1.0 / x;
+#endif
+}
+
 // Stencil position on one axis: clamped coordinate, cell index, weights.
 struct Axis {
     int i;
@@ -176,18 +203,18 @@ struct NsPartials {
 
 TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar, int mode) {
     const double md = (double)mode;
-    const double Np2 = Npar * Npar, Y2 = Y * Y, invY2 = 1.0 / Y2;
+    const double Np2 = Npar * Npar, Y2 = Y * Y, invY = rcp_nz(Y), invY2 = invY * invY;
     const double om = 1.0 - Np2, omX = 1.0 - X;
     const double Delta = om * om + 4.0 * Np2 * omX * invY2;
     const double sq = sqrt(Delta);
     const double A = 1.0 + md * sq + Np2;
     const double Q = 2.0 * (-1.0 + X + Y2);
-    const double invQ = 1.0 / Q;
+    const double invQ = rcp_nz(Q);
     const double G = X * Y2 * invQ;
     const double dDel_dX = -4.0 * Np2 * invY2;
-    const double dDel_dY = -8.0 * Np2 * omX * invY2 / Y;
+    const double dDel_dY = -8.0 * Np2 * omX * invY2 * invY;
     const double dDel_dNp = -4.0 * Npar * om + 8.0 * Npar * omX * invY2;
-    const double h = md * 0.5 / sq;
+    const double h = md * 0.5 * rcp_nz(sq);
     const double dA_dX = h * dDel_dX, dA_dY = h * dDel_dY, dA_dNp = h * dDel_dNp + 2.0 * Npar;
     const double invQ2 = invQ * invQ;
     const double dG_dX = 2.0 * Y2 * (Y2 - 1.0) * invQ2;
@@ -203,7 +230,7 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
 // Plasma parameters at a point, with Cartesian gradients (eval_plasma,
 // src/dispersion.jl:7-15; B_spline/n_e/T_e, src/plasma.jl:73-89).
 struct PlasmaPoint {
-    double X, Y, b[3], Babs, B[3], ne;
+    double X, Y, b[3], Babs, invB, B[3], ne;
     double lnTe, psi;
     // gradients wrt x (Cartesian)
     double dX[3], dY[3];
@@ -227,7 +254,7 @@ template <bool WITH_TE>
 TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
     const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
-    const double invR = 1.0 / R;
+    const double invR = rcp_nz(R);
     const double c = x[0] * invR, s = x[1] * invR;
     constexpr int NV = WITH_TE ? 1 : 0;
     FieldPack<4, NV> f;
@@ -257,8 +284,9 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     p.B[1] = By;
     p.B[2] = Bz;
     const double Babs = sqrt(Bx * Bx + By * By + Bz * Bz);
-    const double invB = 1.0 / Babs;
+    const double invB = rcp_nz(Babs);
     p.Babs = Babs;
+    p.invB = invB;
     p.b[0] = Bx * invB;
     p.b[1] = By * invB;
     p.b[2] = Bz * invB;
@@ -284,7 +312,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
     double dDdN[3], dDdx[3];
 #pragma unroll
     for (int q = 0; q < 3; q++) dDdN[q] = 2.0 * N[q] - ns.dNp * p.b[q];
-    const double invB = 1.0 / p.Babs;
+    const double invB = p.invB;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         const double NdB = N[0] * p.dB[q][0] + N[1] * p.dB[q][1] + N[2] * p.dB[q][2];
@@ -293,7 +321,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
         dDdx[q] = -(ns.dX * p.dX[q] + ns.dY * p.dY[q] + ns.dNp * dNpar);
     }
     const double nrm = sqrt(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
-    const double inv = 1.0 / nrm;
+    const double inv = rcp_nz(nrm);
     if (inv_out) *inv_out = inv;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -323,7 +351,7 @@ constexpr double series_coef(int nu, int k) { return inv_fact(k) * inv_fact(k + 
 
 struct GLTable {
     int n;
-    double t[kMaxGL], w[kMaxGL], st[kMaxGL];  // nodes, weights, sqrt(1-t^2)
+    double t[kMaxGL], w[kMaxGL], st[kMaxGL], t2[kMaxGL];  // nodes, weights, sqrt(1-t^2), t^2
 };
 
 #ifndef TORJ_ALBAJAR_NOINLINE
@@ -378,6 +406,8 @@ TORJ_HD void series_pair_loop(double z, double &Sa, double &Sb) {
 // Per-harmonic constants of the node sum (abs_Al_pol_fact / abs_Al_integral_nume_fast)
 struct HarmConst {
     double x_m, K0, K1, K2, K3, K4, K5, upa0, upa1, r2m1, mu;
+    // node-pair form (TORJ_PAIR_V2): gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
+    double C0, C1, C2, hx;
 };
 
 // A symmetric pair of Gauss-Legendre nodes (+t, -t): w * pol_fact * exp(mu (1 -
@@ -491,15 +521,57 @@ TORJ_HD double exp_nonpos(double x) {
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
 #endif
-    return __builtin_amdgcn_ldexp(p, (int)fmax(k, -2000.0));
+    // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
+    // and ldexp of a huge negative exponent underflows to 0
+    int ki;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
+    return __builtin_amdgcn_ldexp(p, ki);
 #else
     return exp(x);
 #endif
 }
 
+#ifndef TORJ_PAIR_V2
+#define TORJ_PAIR_V2 1
+#endif
+#if TORJ_PAIR_V2
+// The two nodes of a pair share every t-even factor.  With
+//   bracket(+-t) = P +- t Q,  P = A (K0 + K3 t^2) - B + Cc K1,  Q = A K4 + Cc K5
+//   gamma(+-t)^2 = (u_par0 +- u_par1 t)^2 + 1 + (r^2-1)(1-t^2) = C0 + C1 t^2 +- C2 t
+// the pair contributes w h^(2m-1) [P (E+ + E-) + t Q (E+ - E-)], E = exp(mu (1 - gamma))
+// -- the same sum as abs_Al_pol_fact x abs_Al_integral_nume_fast's node terms
+// (src/absorption.jl:132-189), regrouped.
 template <int M, int K>
 TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
-                         double w, bool single) {
+                         double w, double t2, bool single) {
+    constexpr double md = (double)M;
+    const double h = c.hx * st;  // half the Bessel argument x_m sqrt(1 - t^2)
+    const double h2 = h * h;
+    double Sm, Sm1;
+    sc.eval(-h2, Sm, Sm1);
+    const double Sl = fma(-h2, Sm1, md * Sm);  // S_{m-1} by the downward recurrence
+    double p = h;  // h^(2m-1)
+#pragma unroll
+    for (int k = 1; k < 2 * M - 1; k++) p *= h;
+    const double hSm = h * Sm;
+    const double A = hSm * Sm;
+    const double T1 = h2 * Sm1;
+    const double B = c.K2 * Sl * (h * T1);
+    const double Cc = st * Sm * (Sl - T1);
+    const double P = fma(A, fma(c.K3, t2, c.K0), fma(Cc, c.K1, -B));
+    const double wp = w * p;
+    const double a = fma(c.C1, t2, c.C0);
+    if (single) return wp * P * exp_nonpos(fma(-c.mu, sqrt_pos(a), c.mu));
+    const double Q = fma(A, c.K4, Cc * c.K5);
+    const double b = c.C2 * t;
+    const double Ep = exp_nonpos(fma(-c.mu, sqrt_pos(a + b), c.mu));
+    const double Em = exp_nonpos(fma(-c.mu, sqrt_pos(a - b), c.mu));
+    return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
+}
+#else
+template <int M, int K>
+TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
+                         double w, double, bool single) {
     constexpr double md = (double)M;
     const double arg = c.x_m * st;
     const double h = 0.5 * arg;
@@ -528,6 +600,7 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double
     }
     return r;
 }
+#endif
 
 template <int M, int K>
 TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
@@ -542,42 +615,45 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
     // chains), with the (uniform, scalar-loaded) node constants of the next U
     // pairs fetched while these compute (gl arrays hold kMaxGL >= half + U
     // entries, so the look-ahead never leaves the table)
-    double tn[U], sn[U], wn[U];
+    double tn[U], sn[U], wn[U], qn[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
         tn[u] = gl.t[u];
         sn[u] = gl.st[u];
         wn[u] = gl.w[u];
+        qn[u] = gl.t2[u];
     }
     int i = 0;
 #pragma unroll 1
     for (; i + U <= half; i += U) {
-        double t[U], st[U], w[U];
+        double t[U], st[U], w[U], q[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             t[u] = tn[u];
             st[u] = sn[u];
             w[u] = wn[u];
+            q[u] = qn[u];
             tn[u] = gl.t[i + U + u];
             sn[u] = gl.st[i + U + u];
             wn[u] = gl.w[i + U + u];
+            qn[u] = gl.t2[i + U + u];
         }
         double r[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) r[u] = pair_term<M, K>(c, sc, t[u], st[u], w[u], false);
+        for (int u = 0; u < U; u++) r[u] = pair_term<M, K>(c, sc, t[u], st[u], w[u], q[u], false);
 #ifdef __HIP_DEVICE_COMPILE__
         // consume the prefetched constants at the END of the iteration, so the
         // s_load latency hides behind these pairs (otherwise load PRE re-rolls
         // them to the loop head, right before their first use)
 #pragma unroll
-        for (int u = 0; u < U; u++) asm volatile("" : "+s"(tn[u]), "+s"(sn[u]), "+s"(wn[u]));
+        for (int u = 0; u < U; u++) asm volatile("" : "+s"(tn[u]), "+s"(sn[u]), "+s"(wn[u]), "+s"(qn[u]));
 #endif
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], false);
-    if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], true);
+    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
+    if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
     double s = acc[0];
 #pragma unroll
     for (int u = 1; u < U; u++) s += acc[u];
@@ -595,23 +671,27 @@ struct AlbajarWork {
 // normalisation a*(mu/2pi)^1.5 (common to both harmonics).
 template <int M>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
-                                double inv_sqNp, double sqNp, double N_perp, double omega_bar,
+                                double inv_sqNp, double N_perp, double omega_bar,
                                 double Axz, double ea, double e3, AlbajarWork *work) {
-    constexpr double md = (double)M;
+    constexpr double md = (double)M, inv_md = 1.0 / md;
     HarmConst c;
     c.r2m1 = r * r - 1.0;
     const double sq_r = sqrt(c.r2m1);
     c.x_m = N_perp * omega_bar * sq_r;
-    const double q = c.x_m / (md * sqNp);
+    const double q = c.x_m * inv_sqNp * inv_md;  // x_m / (m sqrt(1 - N_par^2))
     c.K0 = Axz * Axz + ea * ea;
-    c.K1 = Axz * ea * c.x_m / md;
-    c.K2 = 4.0 * ea * ea / (md * md);
+    c.K1 = Axz * ea * c.x_m * inv_md;
+    c.K2 = 4.0 * ea * ea * (inv_md * inv_md);
     c.K3 = q * q * e3 * e3;
     c.K4 = 2.0 * q * Axz * e3;
-    c.K5 = q * ea * e3 * c.x_m / md;
+    c.K5 = q * ea * e3 * c.x_m * inv_md;
     c.upa0 = inv_sqNp * r * Npar;
     c.upa1 = inv_sqNp * sq_r;
     c.mu = mu;
+    c.C0 = fma(c.upa0, c.upa0, r * r);
+    c.C1 = c.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
+    c.C2 = 2.0 * c.upa0 * c.upa1;
+    c.hx = 0.5 * c.x_m;
     // Series length from the largest Bessel argument x_m (truncation < 2^-58
     // relative, checked with mpmath in tests): x_m <= 1: 9 terms, <= 2: 12,
     // <= 3: 14, <= 4: 16; physical rays have x_m < m.  The level is made
@@ -632,6 +712,8 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
         case 3: sum = node_sum<M, 16>(gl, c); break;
         default: sum = node_sum<M, 0>(gl, c); break;
     }
+    // (m / (N_perp omega_bar))^2: IEEE quotient, N_perp = 0 (parallel
+    // propagation) stays an infinity as in the reference
     const double Pm = md / (N_perp * omega_bar);
     return -mu * Pm * Pm * sum * sq_r;
 }
@@ -639,6 +721,14 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 // abs_Albajar_fast (src/absorption.jl:191-226).  With TORJ_ALBAJAR_NOINLINE the
 // device code keeps it out of line: the RK4 state is then saved once per call
 // instead of competing for registers inside the node loop.
+//
+// Restated for the device (same quantities, fewer instructions):
+//  * sin(acos(cos_t)) is sqrt(1 - cos_t^2) (an fma and a sqrt instead of the
+//    acos and sin library sequences; NaN for |cos_t| > 1 as in the reference,
+//    Appendix A.4);
+//  * quotients by Te, Y, N_abs, Nt, den, sqrt(1 - N_par^2) and the Maxwellian
+//    normalisation use rcp_nz (one reciprocal each, reused), 1/mu = Te e/(m c^2);
+//  * 1 / m_0 = Y / sqrt(1 - N_par^2), 1/(Y c) folded into one product.
 #if defined(__HIP_DEVICE_COMPILE__) && TORJ_ALBAJAR_NOINLINE
 #define TORJ_ALB_ATTR __host__ __device__ __attribute__((noinline))
 #else
@@ -647,64 +737,74 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
                                 double N_par, double Te, int mode, AlbajarWork *work) {
     if (Te < 20.0) return 0.0;
-    const double mu = kMe * kC * kC / (kE * Te);
-    const double omega_bar = 1.0 / Y;
-    const double cos_t = N_par / N_abs;
-    const double sin_t = sin(acos(cos_t));
+    constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te
+    const double inv_mu = Te * (1.0 / kMuTe);
+    const double mu = kMuTe * rcp_nz(Te);
+    const double omega_bar = rcp_nz(Y);
+    const double cos_t = N_par * rcp_nz(N_abs);
+    const double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
     const double N_perp = sqrt(N_abs * N_abs - N_par * N_par);
     // abs_Al_N_with_pol_vec (src/absorption.jl:10-64), real form:
     // e = (e1, i*ea, e3) with e1, ea, e3 real.
     if (X >= 1.0) return 0.0;
     const double s2 = sin_t * sin_t, c2 = cos_t * cos_t, omX = 1.0 - X;
-    double rho = Y * Y * (s2 * s2) + 4.0 * omX * omX * c2;
+    const double Y2 = Y * Y, invY2 = omega_bar * omega_bar;
+    double rho = Y2 * (s2 * s2) + 4.0 * omX * omX * c2;
     if (rho < 0.0) return 0.0;
     rho = sqrt(rho);
-    const double f = (2.0 * omX) / (2.0 * omX - Y * Y * s2 - (double)mode * Y * rho);
+    const double f = (2.0 * omX) * rcp_nz(2.0 * omX - Y2 * s2 - (double)mode * Y * rho);
     double Nt = 1.0 - X * f;
     if (Nt < 0.0) return 0.0;
     Nt = sqrt(Nt);
     if (!(Nt > 0.0) || Nt > 1.0) return 0.0;  // isnan || <= 0 || > 1
-    const double g = 1.0 - (1.0 - Y * Y) * f;
+    const double inv_Nt = rcp_nz(Nt);
+    const double g = 1.0 - (1.0 - Y2) * f;
     double e1 = 0.0, ea = 0.0, e3 = 0.0;
     if (c2 < 1e-5 || 1.0 - s2 < 1e-5) {
         if (mode > 0) {
-            ea = sqrt(1.0 / Nt);
-            e1 = -(1.0 / Y * g) * ea;
+            ea = sqrt(inv_Nt);
+            e1 = -(omega_bar * g) * ea;
         } else {
-            e3 = sqrt(1.0 / Nt);
+            e3 = sqrt(inv_Nt);
         }
     } else {
-        const double den = omX - Nt * Nt * s2;
-        const double ta = 1.0 + ((omX * Nt * Nt * c2) / (den * den)) * 1.0 / (Y * Y) * (g * g);
-        const double tb = 1.0 + (omX / den) * 1.0 / (Y * Y) * (g * g);
+        const double Nt2 = Nt * Nt;
+        const double den = omX - Nt2 * s2;
+        const double inv_den = rcp_nz(den);
+        const double gg = invY2 * (g * g);
+        const double ta = 1.0 + (omX * Nt2 * c2) * (inv_den * inv_den) * gg;
+        const double tb = 1.0 + (omX * inv_den) * gg;
         const double a_sq = s2 * (ta * ta), b_sq = c2 * (tb * tb);
-        ea = sqrt(1.0 / (Nt * sqrt(a_sq + b_sq)));
+        ea = sqrt(inv_Nt * rcp_nz(sqrt(a_sq + b_sq)));
         if (mode <= 0) ea = -ea;
-        e1 = -(1.0 / Y * g) * ea;
-        e3 = -((Nt * Nt * sin_t * cos_t) / den) * e1;
+        e1 = -(omega_bar * g) * ea;
+        e3 = -((Nt2 * sin_t * cos_t) * inv_den) * e1;
     }
-    const double sqNp = sqrt(1.0 - N_par * N_par);
+    const double omNp2 = 1.0 - N_par * N_par;
+    const double sqNp = sqrt(omNp2);
     const double m_0 = sqNp * omega_bar;
-    const double inv_sqNp = 1.0 / sqNp;
-    const double N_eff = (N_perp * N_par) / (1.0 - N_par * N_par);
+    const double inv_sqNp = rcp_nz(sqNp);
+    const double N_eff = (N_perp * N_par) * (inv_sqNp * inv_sqNp);
     const double Axz = e1 + N_eff * e3;
     if (work) work->n_active++;
+    const double inv_m0 = inv_sqNp * Y;
     double c_abs = 0.0;
     if (!(2.0 < m_0)) {
-        c_abs += albajar_harmonic<2>(gl, mu, 2.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
+        c_abs += albajar_harmonic<2>(gl, mu, 2.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
                                      Axz, ea, e3, work);
         if (work) work->n_harm++;
     }
     if (!(3.0 < m_0)) {  // src/absorption.jl:214 `if m < m_0 continue` (NaN m_0 -> NaN, as reference)
-        c_abs += albajar_harmonic<3>(gl, mu, 3.0 / m_0, N_par, inv_sqNp, sqNp, N_perp, omega_bar,
+        c_abs += albajar_harmonic<3>(gl, mu, 3.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
                                      Axz, ea, e3, work);
         if (work) work->n_harm++;
     }
-    const double a = 1.0 / (1.0 + 105.0 / (128.0 * mu * mu) + 15.0 / (8.0 * mu));
-    const double sm = sqrt(mu / (2.0 * kPi));
+    // 1 / (1 + 105/(128 mu^2) + 15/(8 mu)), (mu / 2 pi)^1.5
+    const double a = rcp_nz(fma(inv_mu, fma(inv_mu, 105.0 / 128.0, 15.0 / 8.0), 1.0));
+    const double sm = sqrt(mu * (1.0 / (2.0 * kPi)));
     c_abs *= a * (sm * sm * sm);
-    c_abs = -(c_abs * 2.0 * kPi * kPi / m_0);
-    return c_abs * X * omega / (Y * kC);
+    c_abs = -(c_abs * (2.0 * kPi * kPi) * inv_m0);
+    return c_abs * X * omega * (omega_bar * (1.0 / kC));
 }
 
 // one RHS evaluation of sys! (src/solve.jl:112-114 -> gradΛ!, :85-95)

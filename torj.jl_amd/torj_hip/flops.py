@@ -3,7 +3,8 @@
 Per-component op counts produced by the instrumented restatement
 `python oracle/flopcount.py` (counting convention: add/sub/mul/div/sqrt = 1,
 exp 26, sin/cos 20, acos 30 -- SURVEY.md §8(d)) of the node-pair algorithm the
-kernel runs.  The kernel reports exact work counters per launch (ray-steps, RHS
+kernel runs (the regrouped pair form and reciprocal-based prologue of
+torj_math.hpp: work the kernel no longer does is no longer counted).  The kernel reports exact work counters per launch (ray-steps, RHS
 evaluations, absorption calls that reach the harmonic sum, harmonic integrals,
 Bessel-series terms), so the per-launch figure is exact for the branches
 actually taken.  Absorption calls that exit early (Te < 20 eV, N outside (0,1],
@@ -12,11 +13,11 @@ X >= 1) are counted as zero work (conservative).
 from __future__ import annotations
 
 FLOPS_RHS_COLD = 815        # spline fields + B rotation + analytic dD/dx, dD/dN + Te
-FLOPS_ALPHA_PRE = 135       # abs_Albajar_fast up to the harmonic sum (pol. vector etc.)
-FLOPS_ALPHA_POST = 22       # Maxwellian normalisation + final scaling
-FLOPS_HARM = 36             # per harmonic: K0..K5, u_par coefficients, post-scaling
-FLOPS_PAIR_SHARED = 18      # per +-t node pair: Bessel argument, recurrence, shared factors
-FLOPS_NODE = 46             # per node: bracket, u_par, gamma (sqrt), exp, accumulate
+FLOPS_ALPHA_PRE = 83        # abs_Albajar_fast up to the harmonic sum (pol. vector etc.)
+FLOPS_ALPHA_POST = 17       # Maxwellian normalisation + final scaling
+FLOPS_HARM = 46             # per harmonic: K0..K5, C0..C2, u_par coefficients, post-scaling
+FLOPS_PAIR_SHARED = 35      # per +-t node pair: Bessel argument, recurrence, P, Q, combination
+FLOPS_NODE = 30             # per node: gamma^2, sqrt, exponent, exp
 FLOPS_SERIES_TERM = 4       # per Horner term (two series, one fma each)
 FLOPS_STEP_OVERHEAD = 234   # RK4 combination, exp(-tau), psi evaluation
 
