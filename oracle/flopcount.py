@@ -18,6 +18,7 @@ acos 30 (fdlibm-style polynomial + reduction counts).
 from __future__ import annotations
 
 import math
+import os
 
 COST = {"exp": 26, "sin": 20, "cos": 20, "acos": 30, "sqrt": 1}
 
@@ -182,9 +183,39 @@ def _series_coef(nu, k):
     return 1.0 / (math.factorial(k) * math.factorial(k + nu))
 
 
+_HDR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                    "torj.jl_amd", "csrc", "torj_bessel_coefs.hpp")
+_BT = None
+
+
+def bessel_table():
+    """(terms per level, coef[level][nu-2][k]) parsed from the product's generated
+    header torj_bessel_coefs.hpp (data only; tools/gen_bessel_coefs.py made it)."""
+    global _BT
+    if _BT is None:
+        import re
+        txt = open(_HDR).read()
+        terms = [int(v) for v in re.search(r"kBesselTerms\[kBesselLevels\] = \{([^}]*)\}", txt).group(1).split(",")]
+        body = txt[txt.index("kBesselCoef"):]
+        rows = [[float(v) for v in r.split(",") if v.strip()] for r in re.findall(r"\{([-0-9.e, +]+)\}", body)]
+        coef = [rows[3 * lv:3 * lv + 3] for lv in range(len(terms))]
+        _BT = (terms, coef)
+    return _BT
+
+
+def series_level(x_m):
+    return 0 if x_m <= 1.0 else 1 if x_m <= 2.0 else 2 if x_m <= 3.0 else 3 if x_m <= 4.0 else 4
+
+
 def series_terms(x_m):
-    """series length rule of torj_math.hpp (albajar_harmonic)"""
-    return 9 if x_m <= 1.0 else 12 if x_m <= 2.0 else 14 if x_m <= 3.0 else 16 if x_m <= 4.0 else 44
+    """polynomial length of torj_math.hpp albajar_harmonic for argument x_m"""
+    lv = series_level(x_m)
+    return bessel_table()[0][lv] if lv < 4 else 44
+
+
+def series_coef(nu, k, x_m):
+    lv = series_level(x_m)
+    return bessel_table()[1][lv][nu - 2][k] if lv < 4 else _series_coef(nu, k)
 
 
 def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m, count=None):
@@ -220,10 +251,11 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m
         h2 = h * h
         z = -h2
         n0 = Counter.n
-        Sm, Sm1 = CF(_series_coef(m, K - 1)), CF(_series_coef(m + 1, K - 1))
+        xv = x_m.v
+        Sm, Sm1 = CF(series_coef(m, K - 1, xv)), CF(series_coef(m + 1, K - 1, xv))
         for k in range(K - 2, -1, -1):
-            Sm = Sm * z + _series_coef(m, k)
-            Sm1 = Sm1 * z + _series_coef(m + 1, k)
+            Sm = Sm * z + series_coef(m, k, xv)
+            Sm1 = Sm1 * z + series_coef(m + 1, k, xv)
         n_series = Counter.n - n0
         Sl = md * Sm - h2 * Sm1
         p = h

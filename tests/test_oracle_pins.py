@@ -260,21 +260,28 @@ def test_albajar_cold_and_cut_branches(O):
 
 
 def test_bessel_series_truncation(O):
-    """The GPU's power-series Bessel factors (term counts in torj_math.hpp) are
-    accurate to a few ulp against mpmath for every argument they cover."""
+    """The GPU's Bessel factors (the near-minimax polynomials in z = -(x/2)^2 of
+    torj_bessel_coefs.hpp, tools/gen_bessel_coefs.py) are accurate to a few ulp
+    against mpmath for every argument they cover, like the Taylor series they
+    replace (9 / 12 / 14 / 16 terms)."""
     from mpmath import besselj, mp, mpf
 
     import flopcount as FC
 
     mp.dps = 30
-    for xm_max in (1.0, 2.0, 3.0, 4.0):
+    terms, coef = FC.bessel_table()
+    assert terms == [7, 9, 10, 11]
+    for lv, xm_max in enumerate((1.0, 2.0, 3.0, 4.0)):
         K = FC.series_terms(xm_max)
+        assert K == terms[lv] and FC.series_terms(xm_max + 1e-9) != K
         for nu in (2, 3, 4):
+            c = coef[lv][nu - 2]
+            assert all(v == 0.0 for v in c[K:])
             for x in np.linspace(0.01, xm_max, 23):
                 h2 = (x / 2) ** 2
                 S = 0.0
                 for k in range(K - 1, -1, -1):
-                    S = S * (-h2) + FC._series_coef(nu, k)
+                    S = S * (-h2) + c[k]
                 J = S * (x / 2) ** nu
                 Jr = float(besselj(nu, mpf(x)))
                 assert abs(J - Jr) <= 8 * 2 ** -52 * abs(Jr) + 1e-300, (nu, x, K)  # few-ulp rounding

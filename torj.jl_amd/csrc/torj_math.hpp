@@ -18,6 +18,8 @@
 #include <math.h>
 #include <stdint.h>
 
+#include "torj_bessel_coefs.hpp"
+
 #define TORJ_HD __host__ __device__ __forceinline__
 
 namespace torj {
@@ -82,6 +84,26 @@ TORJ_HD double rcp_nz(double x) {
     return fma(r, e, r);
 #else
     return 1.0 / x;
+#endif
+}
+
+// sqrt of a finite positive normal argument (lengths, |B|, |dD/dN|, the
+// node-loop gamma): on the device v_rsq_f64 + one Goldschmidt step + one Newton
+// correction (~1 ulp; the library sequence adds a second correction for correct
+// rounding plus denormal scaling and class checks).
+#ifndef TORJ_FAST_NODE_MATH
+#define TORJ_FAST_NODE_MATH 1
+#endif
+TORJ_HD double sqrt_pos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+    const double y = __builtin_amdgcn_rsq(x);
+    double g = x * y, h = 0.5 * y;
+    const double r = fma(-h, g, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    return fma(fma(-g, g, x), h, g);
+#else
+    return sqrt(x);
 #endif
 }
 
@@ -253,7 +275,7 @@ TORJ_HD Consts make_consts(double omega) {
 template <bool WITH_TE>
 TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
-    const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
+    const double R = sqrt_pos(x[0] * x[0] + x[1] * x[1]);
     const double invR = rcp_nz(R);
     const double c = x[0] * invR, s = x[1] * invR;
     constexpr int NV = WITH_TE ? 1 : 0;
@@ -283,7 +305,7 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     p.B[0] = Bx;
     p.B[1] = By;
     p.B[2] = Bz;
-    const double Babs = sqrt(Bx * Bx + By * By + Bz * Bz);
+    const double Babs = sqrt_pos(Bx * Bx + By * By + Bz * Bz);
     const double invB = rcp_nz(Babs);
     p.Babs = Babs;
     p.invB = invB;
@@ -320,7 +342,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
         const double dNpar = (NdB - Npar * bdB) * invB;
         dDdx[q] = -(ns.dX * p.dX[q] + ns.dY * p.dY[q] + ns.dNp * dNpar);
     }
-    const double nrm = sqrt(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
+    const double nrm = sqrt_pos(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
     const double inv = rcp_nz(nrm);
     if (inv_out) *inv_out = inv;
 #pragma unroll
@@ -417,38 +439,37 @@ struct HarmConst {
 // S_m, S_{m+1} of K terms + the downward recurrence S_{m-1} = m S_m + z S_{m+1})
 // are computed once per pair.  With `single`, only the +t node is taken (the
 // middle node of an odd-order rule, t = 0).
-#ifndef TORJ_VGPR_COEFS
-#define TORJ_VGPR_COEFS 0
-#endif
 #ifndef TORJ_PAIR_UNROLL
 #define TORJ_PAIR_UNROLL 1
 #endif
 
-// Series coefficients of one harmonic for the node loop.  On the device they are
-// loaded once per harmonic into VGPRs (vector loads through an opaque zero lane
-// offset), so the Horner FMAs take register operands instead of 64-bit literals
-// re-materialised by two s_mov_b32 each per use.
-template <int M, int K>
+// Series coefficients of one harmonic for the node loop (compile-time
+// constants: the Horner FMAs take them as SGPR operands).
+// LV 0..3: the near-minimax polynomials of torj_bessel_coefs.hpp on x_m <= 1, 2,
+// 3, 4 (7 / 9 / 10 / 11 terms; TORJ_BESSEL_ECON=0: the Taylor series, 9 / 12 / 14
+// / 16 terms, same accuracy); LV 4: the 44-term Taylor loop (x_m <= 12).
+#ifndef TORJ_BESSEL_ECON
+#define TORJ_BESSEL_ECON 1
+#endif
+constexpr int kTaylorTerms[4] = {9, 12, 14, kSeriesFast};
+constexpr int series_terms(int lv) {
+    return lv >= 4 ? 0 : (TORJ_BESSEL_ECON ? kBesselTerms[lv] : kTaylorTerms[lv]);
+}
+constexpr double level_coef(int lv, int nu, int k) {
+    return TORJ_BESSEL_ECON ? kBesselCoef[lv][nu - 2][k] : series_coef(nu, k);
+}
+
+template <int M, int LV>
 struct SeriesCoefs {
+    static constexpr int K = series_terms(LV);
     double a[K > 0 ? K : 1], b[K > 0 ? K : 1];
     TORJ_HD void load() {
         if constexpr (K > 0) {
-#if defined(__HIP_DEVICE_COMPILE__) && TORJ_VGPR_COEFS
-            int z;
-            asm volatile("v_mov_b32 %0, 0" : "=v"(z));
-            const double *ta = kSeriesTab.c[M - 2] + z, *tb = kSeriesTab.c[M - 1] + z;
 #pragma unroll
             for (int k = 0; k < K; k++) {
-                a[k] = ta[k];
-                b[k] = tb[k];
+                a[k] = level_coef(LV, M, k);
+                b[k] = level_coef(LV, M + 1, k);
             }
-#else
-#pragma unroll
-            for (int k = 0; k < K; k++) {
-                a[k] = series_coef(M, k);
-                b[k] = series_coef(M + 1, k);
-            }
-#endif
         }
     }
     TORJ_HD void eval(double z, double &Sa, double &Sb) const {
@@ -467,60 +488,28 @@ struct SeriesCoefs {
     }
 };
 
-// Node-loop elementary functions.  On the device: sqrt of a normal positive
-// argument from v_rsq_f64 + one Goldschmidt step + one Newton correction
-// (~1 ulp; the library sequence adds a second correction for correct rounding
-// plus denormal scaling and class checks), and exp of a non-positive argument
-// (range reduction + degree-12 Taylor, ~1 ulp; no overflow path; underflows to
+// Node-loop elementary functions.  exp of a non-positive argument
+// (range reduction + degree-11 near-minimax, ~1 ulp; no overflow path; underflows to
 // 0 through ldexp).  Arguments here: 1 + u^2 >= 1 and mu (1 - gamma) <= 0.
-#ifndef TORJ_FAST_NODE_MATH
-#define TORJ_FAST_NODE_MATH 1
-#endif
-#ifndef TORJ_EXP_ESTRIN
-#define TORJ_EXP_ESTRIN 0
-#endif
-TORJ_HD double sqrt_pos(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
-    const double y = __builtin_amdgcn_rsq(x);
-    double g = x * y, h = 0.5 * y;
-    const double r = fma(-h, g, 0.5);
-    g = fma(g, r, g);
-    h = fma(h, r, h);
-    return fma(fma(-g, g, x), h, g);
-#else
-    return sqrt(x);
-#endif
-}
 TORJ_HD double exp_nonpos(double x) {
 #if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
     const double k = __builtin_rint(x * 1.4426950408889634074);
     double r = fma(-k, 6.93147180559945286227e-01, x);
     r = fma(-k, 2.31904681384629955842e-17, r);
-#if TORJ_EXP_ESTRIN
-    // Estrin form: depth 5 instead of 12 (more independent work per wave)
-    const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-    const double a0 = fma(r, 1.0, 1.0), a1 = fma(r, 1.0 / 6.0, 0.5);
-    const double a2 = fma(r, 1.0 / 120.0, 1.0 / 24.0), a3 = fma(r, 1.0 / 5040.0, 1.0 / 720.0);
-    const double a4 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0);
-    const double a5 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0);
-    const double b0 = fma(r2, a1, a0), b1 = fma(r2, a3, a2), b2 = fma(r2, a5, a4);
-    const double c1 = fma(r4, 1.0 / 479001600.0, b2);
-    const double p = fma(r8, c1, fma(r4, b1, b0));
-#else
-    double p = 1.0 / 479001600.0;  // 1/12!
-    p = fma(p, r, 1.0 / 39916800.0);
-    p = fma(p, r, 1.0 / 3628800.0);
-    p = fma(p, r, 1.0 / 362880.0);
-    p = fma(p, r, 1.0 / 40320.0);
-    p = fma(p, r, 1.0 / 5040.0);
-    p = fma(p, r, 1.0 / 720.0);
-    p = fma(p, r, 1.0 / 120.0);
-    p = fma(p, r, 1.0 / 24.0);
-    p = fma(p, r, 1.0 / 6.0);
-    p = fma(p, r, 0.5);
+    // degree 11 near-minimax on |r| <= ln2/2 (tools/gen_exp_poly.py: 0.58 ulp,
+    // against 1.5 ulp for the degree 12 Taylor polynomial)
+    double p = 2.5100375832561234e-08;
+    p = fma(p, r, 2.7620075879983367e-07);
+    p = fma(p, r, 2.7557268480310024e-06);
+    p = fma(p, r, 2.4801521322368692e-05);
+    p = fma(p, r, 0.00019841269863040545);
+    p = fma(p, r, 0.0013888888917196719);
+    p = fma(p, r, 0.008333333333330065);
+    p = fma(p, r, 0.041666666666624164);
+    p = fma(p, r, 0.16666666666666669);
+    p = fma(p, r, 0.5000000000000001);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
-#endif
     // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
     // and ldexp of a huge negative exponent underflows to 0
     int ki;
@@ -541,8 +530,8 @@ TORJ_HD double exp_nonpos(double x) {
 // the pair contributes w h^(2m-1) [P (E+ + E-) + t Q (E+ - E-)], E = exp(mu (1 - gamma))
 // -- the same sum as abs_Al_pol_fact x abs_Al_integral_nume_fast's node terms
 // (src/absorption.jl:132-189), regrouped.
-template <int M, int K>
-TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
+template <int M, int LV>
+TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double st,
                          double w, double t2, bool single) {
     constexpr double md = (double)M;
     const double h = c.hx * st;  // half the Bessel argument x_m sqrt(1 - t^2)
@@ -569,8 +558,8 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double
     return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 #else
-template <int M, int K>
-TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double t, double st,
+template <int M, int LV>
+TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double st,
                          double w, double, bool single) {
     constexpr double md = (double)M;
     const double arg = c.x_m * st;
@@ -602,9 +591,9 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, K> &sc, double
 }
 #endif
 
-template <int M, int K>
+template <int M, int LV>
 TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
-    SeriesCoefs<M, K> sc;
+    SeriesCoefs<M, LV> sc;
     sc.load();
     const int n = gl.n, half = n >> 1;
     constexpr int U = TORJ_PAIR_UNROLL;
@@ -640,7 +629,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
         }
         double r[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) r[u] = pair_term<M, K>(c, sc, t[u], st[u], w[u], q[u], false);
+        for (int u = 0; u < U; u++) r[u] = pair_term<M, LV>(c, sc, t[u], st[u], w[u], q[u], false);
 #ifdef __HIP_DEVICE_COMPILE__
         // consume the prefetched constants at the END of the iteration, so the
         // s_load latency hides behind these pairs (otherwise load PRE re-rolls
@@ -652,8 +641,8 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, K>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
-    if (n & 1) acc[0] += pair_term<M, K>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
+    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
+    if (n & 1) acc[0] += pair_term<M, LV>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
     double s = acc[0];
 #pragma unroll
     for (int u = 1; u < U; u++) s += acc[u];
@@ -692,25 +681,26 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     c.C1 = c.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
     c.C2 = 2.0 * c.upa0 * c.upa1;
     c.hx = 0.5 * c.x_m;
-    // Series length from the largest Bessel argument x_m (truncation < 2^-58
-    // relative, checked with mpmath in tests): x_m <= 1: 9 terms, <= 2: 12,
-    // <= 3: 14, <= 4: 16; physical rays have x_m < m.  The level is made
+    // Bessel polynomial from the largest argument x_m (SeriesCoefs: x_m <= 1,
+    // 2, 3, 4, each within a few ulp of mpmath's J_nu, checked in tests; the
+    // 44-term Taylor loop beyond); physical rays have x_m < m.  The level is made
     // wave-uniform (max over the active lanes) so the node loop does not diverge.
     int level = c.x_m <= 1.0 ? 0 : (c.x_m <= 2.0 ? 1 : (c.x_m <= 3.0 ? 2 : (c.x_m <= kArgFast ? 3 : 4)));
 #ifdef __HIP_DEVICE_COMPILE__
     level = __ballot(level == 4) ? 4 : (__ballot(level == 3) ? 3 : (__ballot(level == 2) ? 2 : (__ballot(level == 1) ? 1 : 0)));
 #endif
     if (work) {
-        constexpr int kTerms[5] = {9, 12, 14, kSeriesFast, kSeriesSlow};
+        constexpr int kTerms[5] = {series_terms(0), series_terms(1), series_terms(2), series_terms(3),
+                                   kSeriesSlow};
         work->n_terms += (uint32_t)(kTerms[level] * ((gl.n + 1) >> 1));
     }
     double sum;
     switch (level) {
-        case 0: sum = node_sum<M, 9>(gl, c); break;
-        case 1: sum = node_sum<M, 12>(gl, c); break;
-        case 2: sum = node_sum<M, 14>(gl, c); break;
-        case 3: sum = node_sum<M, 16>(gl, c); break;
-        default: sum = node_sum<M, 0>(gl, c); break;
+        case 0: sum = node_sum<M, 0>(gl, c); break;
+        case 1: sum = node_sum<M, 1>(gl, c); break;
+        case 2: sum = node_sum<M, 2>(gl, c); break;
+        case 3: sum = node_sum<M, 3>(gl, c); break;
+        default: sum = node_sum<M, 4>(gl, c); break;
     }
     // (m / (N_perp omega_bar))^2: IEEE quotient, N_perp = 0 (parallel
     // propagation) stays an infinity as in the reference
@@ -762,10 +752,10 @@ TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X,
     double e1 = 0.0, ea = 0.0, e3 = 0.0;
     if (c2 < 1e-5 || 1.0 - s2 < 1e-5) {
         if (mode > 0) {
-            ea = sqrt(inv_Nt);
+            ea = sqrt_pos(inv_Nt);
             e1 = -(omega_bar * g) * ea;
         } else {
-            e3 = sqrt(inv_Nt);
+            e3 = sqrt_pos(inv_Nt);
         }
     } else {
         const double Nt2 = Nt * Nt;
@@ -775,7 +765,7 @@ TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X,
         const double ta = 1.0 + (omX * Nt2 * c2) * (inv_den * inv_den) * gg;
         const double tb = 1.0 + (omX * inv_den) * gg;
         const double a_sq = s2 * (ta * ta), b_sq = c2 * (tb * tb);
-        ea = sqrt(inv_Nt * rcp_nz(sqrt(a_sq + b_sq)));
+        ea = sqrt_pos(inv_Nt * rcp_nz(sqrt_pos(a_sq + b_sq)));
         if (mode <= 0) ea = -ea;
         e1 = -(omega_bar * g) * ea;
         e3 = -((Nt2 * sin_t * cos_t) * inv_den) * e1;
@@ -801,7 +791,7 @@ TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X,
     }
     // 1 / (1 + 105/(128 mu^2) + 15/(8 mu)), (mu / 2 pi)^1.5
     const double a = rcp_nz(fma(inv_mu, fma(inv_mu, 105.0 / 128.0, 15.0 / 8.0), 1.0));
-    const double sm = sqrt(mu * (1.0 / (2.0 * kPi)));
+    const double sm = sqrt_pos(mu * (1.0 / (2.0 * kPi)));
     c_abs *= a * (sm * sm * sm);
     c_abs = -(c_abs * (2.0 * kPi * kPi) * inv_m0);
     return c_abs * X * omega * (omega_bar * (1.0 / kC));
@@ -817,7 +807,7 @@ TORJ_HD void ray_rhs(const double *__restrict__ coef, const Grid &g, const Const
     double Npar;
     dispersion_grad(p, N, mode, du, &Npar);
     if constexpr (ABS) {
-        const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
+        const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
     } else {
         alpha = 0.0;
