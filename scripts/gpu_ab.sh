@@ -6,12 +6,6 @@ ARGS=$1; shift
 mkdir -p gpurun_out/ab
 for v in "$@"; do
   if [ "$v" = main ]; then L=torj.jl_amd/build/libtorj_hip.so; else L=torj.jl_amd/build/variants/libtorj_hip_$v.so; fi
-  TORJ_HIP_LIB=$L timeout -k 10 400 python bench.py --no-cpu-baseline $ARGS > gpurun_out/ab/$v.log 2>&1 || { tail -20 gpurun_out/ab/$v.log; exit 1; }
-  python - gpurun_out/ab/$v.log $v <<'PY'
-import json, sys
-for l in open(sys.argv[1]):
-    if l.startswith("{"):
-        d = json.loads(l); r = d["roofline"]
-        print(f"{sys.argv[2]}: value {d['value']:.4e} kernel {r['kernel_ms']:.1f} ms")
-PY
+  TORJ_HIP_LIB=$PWD/$L timeout -k 10 400 python bench.py --no-cpu-baseline $ARGS > gpurun_out/ab/$v.log 2>&1 || { tail -20 gpurun_out/ab/$v.log; exit 1; }
+  echo -n "$v: "; python tools/bench_brief.py gpurun_out/ab/$v.log
 done

@@ -44,56 +44,66 @@ struct FitArgs {
     const double *s0;        // n, vacuum path length to the entry point
     const int *steps;        // n
     const double *smp_psi, *smp_dpds, *smp_s;  // (n_steps + 1) x n (smp_s: arc length s_k)
-    double *cp, *Mpsi, *MP;            // (n_steps + 2) x n Thomas / second derivatives
-    unsigned char *cnt;                // n_psi x n root counts per boundary
-    double *Fopen;                     // (n_psi - 1) x n: F at a shell's open root, NaN = closed
+    int s_uniform;                     // fixed-step RK4: s_k = s0 + k ds (smp_s unused)
+    double *E, *Gpsi, *GP;             // (n_steps + 2) x n backward-elimination coefficients
+    int *cnt;                          // (n_psi + 1) x n root-count differences per boundary
+    double *Fopen;                     // (n_psi - 1) x n: F at a spilled open shell's root, NaN = closed
     double *dPs;                       // (n_psi - 1) x n: per-ray shell powers (before the break)
     int *kstar;                        // n: break shell
     double *dP;                        // n_psi + 1 (weighted sums; written by k_shell_sum)
     double *Pray;                      // n: per-ray deposited power (reference's P)
 };
 
-constexpr int kChunk = 8;  // points per prefetch batch of the sequential sweeps
+constexpr int kChunk = 8;      // points per prefetch batch of the sequential sweeps
+constexpr int kWalkChunk = 4;  // the walk's batch (five streams, the heavy segment code)
 
 struct RayData {
     const FitArgs *a;
     int i, m;  // lane's ray, number of points (steps + 2)
     double s0, psiL;
-    __device__ double S(int j) const { return j == 0 ? 0.0 : a->smp_s[(size_t)(j - 1) * a->n + i]; }
+    // arc length of point j: 0 (launch), s0 (entry), s0 + (j-1) ds for RK4 (the
+    // fma the trajectory output uses), else the integrator's stored s
+    __device__ double S(int j) const {
+        if (j == 0) return 0.0;
+        return a->s_uniform ? fma((double)(j - 1), a->ds, s0) : a->smp_s[(size_t)(j - 1) * a->n + i];
+    }
     __device__ double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
     __device__ double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[(size_t)(j - 1) * a->n + i]; }
     __device__ double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[(size_t)(j - 1) * a->n + i]; }
-    __device__ double &CP(int j) const { return a->cp[(size_t)j * a->n + i]; }
-    __device__ double &MPSI(int j) const { return a->Mpsi[(size_t)j * a->n + i]; }
-    __device__ double &MPP(int j) const { return a->MP[(size_t)j * a->n + i]; }
+    __device__ double &EE(int j) const { return a->E[(size_t)j * a->n + i]; }
+    __device__ double &GPSI(int j) const { return a->Gpsi[(size_t)j * a->n + i]; }
+    __device__ double &GPP(int j) const { return a->GP[(size_t)j * a->n + i]; }
 };
 
 // not-a-knot cubic interpolation of psi and dP/ds (m >= 4 points): second
 // derivatives M_j.  Rows r = 1..m-2 of the usual tridiagonal system, with
 // M_0 = (1 + h0/h1) M_1 - (h0/h1) M_2 (third-derivative continuity at s_1)
-// folded into row 1 and the mirror relation into row m-2.
-__device__ void nak_solve(const RayData &R) {
+// folded into row 1 and the mirror relation into row m-2.  Eliminated from the
+// bottom up (this sweep stores e_r, g_r with M_r = g_r - e_r M_{r-1}), so the
+// substitution runs upwards in s and fuses with the root walk (walk_ray): one
+// stored sweep instead of two.
+__device__ __forceinline__ void nak_eliminate(const RayData &R) {
     const int m = R.m;
-    double cprev = 0.0, dpsi = 0.0, dPp = 0.0;
-    double yl = R.Ypsi(0), yc = R.Ypsi(1), Pl = R.YP(0), Pc = R.YP(1);
-    double hl = R.h(0);
     const double h0 = R.h(0), h1 = R.h(1), hm2 = R.h(m - 2), hm3 = R.h(m - 3);
-    for (int r0 = 1; r0 <= m - 2; r0 += kChunk) {
+    double yn = R.Ypsi(m - 1), yc = R.Ypsi(m - 2), Pn = R.YP(m - 1), Pc = R.YP(m - 2);
+    double hr = R.h(m - 2), ihr = rcp_nz(hr);
+    double e = 0.0, gp = 0.0, gP = 0.0;
+    for (int r0 = m - 2; r0 >= 1; r0 -= kChunk) {
         double yv[kChunk], Pv[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
-            const int j = min(r0 + 1 + u, m - 1);
+            const int j = max(r0 - 1 - u, 0);
             yv[u] = R.Ypsi(j);
             Pv[u] = R.YP(j);
         }
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
-            const int r = r0 + u;
-            if (r > m - 2) break;
-            const double hr = R.h(r);
-            const double yn = yv[u], Pn = Pv[u];
-            const double rp = 6.0 * ((yn - yc) / hr - (yc - yl) / hl);
-            const double rP = 6.0 * ((Pn - Pc) / hr - (Pc - Pl) / hl);
+            const int r = r0 - u;
+            if (r < 1) break;
+            const double hl = R.h(r - 1), ihl = rcp_nz(hl);
+            const double yl = yv[u], Pl = Pv[u];
+            const double rp = 6.0 * ((yn - yc) * ihr - (yc - yl) * ihl);
+            const double rP = 6.0 * ((Pn - Pc) * ihr - (Pc - Pl) * ihl);
             double sub = hl, dia = 2.0 * (hl + hr), sup = hr;
             if (r == 1) {
                 dia = 3.0 * h0 + 2.0 * h1 + h0 * h0 / h1;
@@ -102,44 +112,19 @@ __device__ void nak_solve(const RayData &R) {
             }
             if (r == m - 2) {
                 sub = hm3 - hm2 * hm2 / hm3;
-                dia = (r == 1) ? dia : 2.0 * hm3 + 3.0 * hm2 + hm2 * hm2 / hm3;
+                dia = 2.0 * hm3 + 3.0 * hm2 + hm2 * hm2 / hm3;
                 sup = 0.0;
             }
-            const double den = dia - sub * cprev;
-            cprev = sup / den;
-            dpsi = (rp - sub * dpsi) / den;
-            dPp = (rP - sub * dPp) / den;
-            R.CP(r) = cprev;
-            R.MPSI(r) = dpsi;
-            R.MPP(r) = dPp;
-            yl = yc, yc = yn, Pl = Pc, Pc = Pn, hl = hr;
+            const double iden = rcp_nz(dia - sup * e);  // e = e_{r+1} (0 below row m-2)
+            gp = (rp - sup * gp) * iden;
+            gP = (rP - sup * gP) * iden;
+            e = sub * iden;
+            R.EE(r) = e;
+            R.GPSI(r) = gp;
+            R.GPP(r) = gP;
+            yn = yc, yc = yl, Pn = Pc, Pc = Pl, hr = hl, ihr = ihl;
         }
     }
-    double Mp = R.MPSI(m - 2), MPn = R.MPP(m - 2);
-    for (int r0 = m - 3; r0 >= 1; r0 -= kChunk) {
-        double cv[kChunk], dv[kChunk], ev[kChunk];
-#pragma unroll
-        for (int u = 0; u < kChunk; u++) {
-            const int r = max(r0 - u, 1);
-            cv[u] = R.CP(r);
-            dv[u] = R.MPSI(r);
-            ev[u] = R.MPP(r);
-        }
-#pragma unroll
-        for (int u = 0; u < kChunk; u++) {
-            const int r = r0 - u;
-            if (r < 1) break;
-            Mp = dv[u] - cv[u] * Mp;
-            MPn = ev[u] - cv[u] * MPn;
-            R.MPSI(r) = Mp;
-            R.MPP(r) = MPn;
-        }
-    }
-    const double q0 = h0 / h1, q1 = hm2 / hm3;
-    R.MPSI(0) = (1.0 + q0) * R.MPSI(1) - q0 * R.MPSI(2);
-    R.MPP(0) = (1.0 + q0) * R.MPP(1) - q0 * R.MPP(2);
-    R.MPSI(m - 1) = (1.0 + q1) * R.MPSI(m - 2) - q1 * R.MPSI(m - 3);
-    R.MPP(m - 1) = (1.0 + q1) * R.MPP(m - 2) - q1 * R.MPP(m - 3);
 }
 
 struct Cubic {  // y0 + t (b + t (c + t d)), t in [0, h]
@@ -190,11 +175,11 @@ struct Cursor {
     const FitArgs *a;
     int c;
     double lo, hi;  // grid[c-1] (or -inf), grid[c] (or +inf)
-    __device__ void load() {
+    __device__ __forceinline__ void load() {
         lo = c > 0 ? a->grid[c - 1] : -INFINITY;
         hi = c < a->n_psi ? a->grid[c] : INFINITY;
     }
-    __device__ void seek(double v) {  // c = #boundaries <= v
+    __device__ __forceinline__ void seek(double v) {  // c = #boundaries <= v
         if (v >= lo && v < hi) return;
         while (c < a->n_psi && a->grid[c] <= v) c++;
         while (c > 0 && a->grid[c - 1] > v) c--;
@@ -221,42 +206,105 @@ __device__ double cubic_root(const Cubic &q, double L, double ta, double tb, boo
     return t;
 }
 
+// Per-root state without per-root memory traffic (a wave's lanes sit at
+// different boundaries, so every per-root access is 64 scattered lines):
+//  * open shells (one root seen, waiting for its partner) live in a small
+//    register cache; a third open shell spills the oldest entry to Fopen;
+//  * root counts are kept as runs: consecutive roots at k, k+d, k+2d, ... (a
+//    monotone crossing of the boundary levels) form one run, flushed as a
+//    difference pair cdiff[lo] += 1, cdiff[hi + 1] -= 1, so cnt[k] is a prefix
+//    sum (one flush per turning point of psi(s), not one update per root);
+//  * a closed pair adds its |integral| to the shell (TORJ_DEPO_ATOMIC: no-return
+//    atomic; else a plain read-modify-write of the lane's own element).
+#ifndef TORJ_DEPO_ATOMIC
+#define TORJ_DEPO_ATOMIC 1
+#endif
+constexpr int kOpenCache = 2;
+
 struct Walker {
     const FitArgs *a;
     int i;
     double Fhi, Flo;  // compensated running integral of dP/ds at the segment start
     Cursor cur;
-    // a root of boundary L_k at running integral Fr: count it and toggle the
-    // shells it bounds (k-1 above it, k below it)
-    __device__ void root(int k, double Fr) {
-        unsigned char &c = a->cnt[(size_t)k * a->n + i];
-        if (c < 255) c++;
+    int oq[kOpenCache];     // open shell ids (-1: free slot)
+    double oF[kOpenCache];  // F at their opening root
+    bool spilled;           // some open shell lives in Fopen
+    int run_k0, run_k1, run_d;  // current run of roots (run_d = 0: none)
+    __device__ __forceinline__ void init() {
 #pragma unroll
-        for (int dq = -1; dq <= 0; dq++) {
-            const int q = k + dq;
-            if (q < 0 || q > a->n_psi - 2) continue;
-            double &fo = a->Fopen[(size_t)q * a->n + i];
-            if (isnan(fo)) {
-                fo = Fr;
-            } else {
-                a->dPs[(size_t)q * a->n + i] += fabs(Fr - fo);  // |integrate(dP_ds, r1, r2)|
-                fo = NAN;
-            }
+        for (int u = 0; u < kOpenCache; u++) oq[u] = -1, oF[u] = 0.0;
+        spilled = false;
+        run_d = 0, run_k0 = run_k1 = 0;
+    }
+    __device__ __forceinline__ void cadd(int k, int v) {
+        __hip_atomic_fetch_add(a->cnt + (size_t)k * a->n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __device__ __forceinline__ void flush_run() {
+        if (run_d == 0) return;
+        const int lo = run_k0 < run_k1 ? run_k0 : run_k1, hi = run_k0 < run_k1 ? run_k1 : run_k0;
+        cadd(lo, 1);
+        cadd(hi + 1, -1);
+        run_d = 0;
+    }
+    __device__ __forceinline__ void close(int q, double d) {  // |integrate(dP_ds, r1, r2)|
+        double *p = a->dPs + (size_t)q * a->n + i;
+#if TORJ_DEPO_ATOMIC
+        __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+        *p += d;
+#endif
+    }
+    __device__ __forceinline__ void toggle(int q, double Fr) {
+        bool hit = false;
+        double fo = 0.0;
+#pragma unroll
+        for (int u = 0; u < kOpenCache; u++)
+            if (!hit && oq[u] == q) hit = true, fo = oF[u], oq[u] = -1;
+        if (!hit && spilled) {  // maybe open in memory
+            double &m = a->Fopen[(size_t)q * a->n + i];
+            fo = m;
+            if (!isnan(fo)) hit = true, m = NAN;
         }
+        if (hit) {
+            close(q, fabs(Fr - fo));
+            return;
+        }
+        bool placed = false;
+#pragma unroll
+        for (int u = 0; u < kOpenCache; u++)
+            if (!placed && oq[u] < 0) placed = true, oq[u] = q, oF[u] = Fr;
+        if (!placed) {  // spill slot 0 (rare: > 2 shells open at once)
+            a->Fopen[(size_t)oq[0] * a->n + i] = oF[0];
+            spilled = true;
+            oq[0] = q, oF[0] = Fr;
+        }
+    }
+    // a root of boundary L_k at running integral Fr, found while the boundary
+    // levels are crossed in direction d (+1 upwards, -1 downwards): count it and
+    // toggle the shells it bounds (k-1 above it, k below it)
+    __device__ __forceinline__ void root(int k, double Fr, int d) {
+        if (d == run_d && k == run_k1 + d) {
+            run_k1 = k;
+        } else {
+            flush_run();
+            run_d = d, run_k0 = run_k1 = k;
+        }
+        if (k - 1 >= 0 && k - 1 <= a->n_psi - 2) toggle(k - 1, Fr);
+        if (k <= a->n_psi - 2) toggle(k, Fr);
     }
 };
 
 // stream segment j of the psi spline: every boundary crossing in s order.
 // End values are the data (y0, y1), so a boundary equal to a data value is
 // found exactly once: roots lie in (s_j, s_{j+1}] (segment 0 also takes s = 0).
-__device__ void walk_segment(Walker &W, const Cubic &qs, double y1, const Cubic &qP, bool first) {
+// The segment splits at the zeros of psi' into at most three monotone pieces
+// [0, c1], [c1, c2], [c2, h] (absent cuts sit at h and give empty pieces); one
+// rolled piece loop and one root loop keep the code (and registers) small.
+__device__ __forceinline__ void walk_segment(Walker &W, const Cubic &qs, double y1, const Cubic &qP, bool first) {
     const FitArgs &a = *W.a;
-    // fast path: no boundary between the end values and a monotone segment
     const double A = 3.0 * qs.d, B = 2.0 * qs.c, C = qs.b;
     const double disc = B * B - 4.0 * A * C;
-    double cut[4];
-    int nc = 0;
-    cut[nc++] = 0.0;
+    double c1 = qs.h, c2 = qs.h;
     if (A != 0.0 ? disc > 0.0 : B != 0.0) {  // psi'(t) may vanish inside: split there
         double r1 = NAN, r2 = NAN;
         if (A != 0.0) {
@@ -272,35 +320,44 @@ __device__ void walk_segment(Walker &W, const Cubic &qs, double y1, const Cubic 
             r1 = r2;
             r2 = t;
         }
-        if (r1 > 0.0 && r1 < qs.h) cut[nc++] = r1;
-        if (r2 > 0.0 && r2 < qs.h && r2 != r1) cut[nc++] = r2;
+        const bool in1 = r1 > 0.0 && r1 < qs.h, in2 = r2 > 0.0 && r2 < qs.h && r2 != r1;
+        if (in1) c1 = r1;
+        if (in2) {
+            if (in1)
+                c2 = r2;
+            else
+                c1 = r2;
+        }
     }
-    cut[nc++] = qs.h;
-    double fa = qs.y0;
-    for (int p = 0; p + 1 < nc; p++) {
-        const double ta = cut[p], tb = cut[p + 1];
-        const double fb = (p + 2 == nc) ? y1 : qs.f(tb);
+    double fa = qs.y0, ta = 0.0;
+#pragma unroll 1
+    for (int p = 0; p < 3; p++) {
+        const double tb = p == 0 ? c1 : (p == 1 ? c2 : qs.h);
+        if (!(tb > ta) && p > 0) continue;  // empty piece (absent cut)
+        const double fb = (tb == qs.h) ? y1 : qs.f(tb);
+        const bool first0 = first && p == 0;
+        int k, kend, d;
         if (fb > fa) {  // increasing: boundaries fa < L <= fb (fa <= L at s = 0), ascending
-            int k = (first && p == 0) ? level_above(a, fa, false) : W.cur.c;
+            d = 1;
+            k = first0 ? level_above(a, fa, false) : W.cur.c;
             W.cur.seek(fb);
-            for (; k < W.cur.c; k++) {
-                const double L = a.grid[k];
-                const double t = (L == fb) ? tb : (L == fa ? ta : cubic_root(qs, L, ta, tb, true));
-                W.root(k, W.Fhi + (W.Flo + qP.G(t)));
-            }
+            kend = W.cur.c;
         } else if (fb < fa) {  // decreasing: boundaries fb <= L < fa (<= fa at s = 0), descending
-            const int top = (first && p == 0) ? level_above(a, fa, true) : W.cur.c - (fa == W.cur.lo);
+            d = -1;
+            k = (first0 ? level_above(a, fa, true) : W.cur.c - (fa == W.cur.lo)) - 1;
             W.cur.seek(fb);
-            const int bot = W.cur.c - (fb == W.cur.lo);  // #boundaries < fb
-            for (int k = top - 1; k >= bot; k--) {
-                const double L = a.grid[k];
-                const double t = (L == fb) ? tb : (L == fa ? ta : cubic_root(qs, L, ta, tb, false));
-                W.root(k, W.Fhi + (W.Flo + qP.G(t)));
-            }
+            kend = W.cur.c - (fb == W.cur.lo) - 1;  // #boundaries < fb, minus one
         } else {
             W.cur.seek(fb);
+            d = 0, k = kend = 0;
         }
-        fa = fb;
+        for (; d > 0 ? k < kend : k > kend; k += d) {
+            const double L = a.grid[k];
+            const double t = (L == fb) ? tb : (L == fa ? ta : cubic_root(qs, L, ta, tb, d > 0));
+            W.root(k, W.Fhi + (W.Flo + qP.G(t)), d);
+        }
+        fa = fb, ta = tb;
+        if (tb == qs.h) break;
     }
     // F(s_{j+1}) = F(s_j) + integral over the segment (TwoSum compensation)
     const double g = qP.G(qs.h);
@@ -310,28 +367,48 @@ __device__ void walk_segment(Walker &W, const Cubic &qs, double y1, const Cubic 
     W.Fhi = sum;
 }
 
-__device__ void walk_ray(Walker &W, const RayData &R) {
-    double yl = R.Ypsi(0), Pl = R.YP(0), Ml = R.MPSI(0), MPl = R.MPP(0);
+// the root walk over the segments, with the spline's second derivatives from
+// the upward substitution M_r = g_r - e_r M_{r-1} (nak_eliminate) as it goes
+__device__ __forceinline__ void walk_ray(Walker &W, const RayData &R) {
+    const int m = R.m;
+    const double q0 = R.h(0) / R.h(1), q1 = R.h(m - 2) / R.h(m - 3);
+    const double M1 = R.GPSI(1), M1P = R.GPP(1);
+    const double M2 = R.GPSI(2) - R.EE(2) * M1, M2P = R.GPP(2) - R.EE(2) * M1P;
+    // segment j uses (M_j, M_{j+1}); M_{j+2} is prepared for the next one
+    double Ml = (1.0 + q0) * M1 - q0 * M2, MPl = (1.0 + q0) * M1P - q0 * M2P;
+    double Mr = M1, MPr = M1P, Mn = M2, MPn = M2P;
+    double yl = R.Ypsi(0), Pl = R.YP(0);
     W.cur.c = level_above(*W.a, yl, true);  // #boundaries <= psi(s = 0)
     W.cur.load();
-    for (int j0 = 0; j0 + 1 < R.m; j0 += kChunk) {
-        double yv[kChunk], Pv[kChunk], Mv[kChunk], MPv[kChunk];
+    for (int j0 = 0; j0 + 1 < m; j0 += kWalkChunk) {
+        double yv[kWalkChunk], Pv[kWalkChunk], ev[kWalkChunk], gv[kWalkChunk], gPv[kWalkChunk];
 #pragma unroll
-        for (int u = 0; u < kChunk; u++) {
-            const int j = min(j0 + 1 + u, R.m - 1);
+        for (int u = 0; u < kWalkChunk; u++) {
+            const int j = min(j0 + 1 + u, m - 1);
             yv[u] = R.Ypsi(j);
             Pv[u] = R.YP(j);
-            Mv[u] = R.MPSI(j);
-            MPv[u] = R.MPP(j);
+            const int r = min(j0 + 3 + u, m - 2);  // row of M_{j+3}, prepared after segment j+1
+            ev[u] = R.EE(r);
+            gv[u] = R.GPSI(r);
+            gPv[u] = R.GPP(r);
         }
 #pragma unroll
-        for (int u = 0; u < kChunk; u++) {
+        for (int u = 0; u < kWalkChunk; u++) {
             const int j = j0 + u;
-            if (j + 1 >= R.m) break;
+            if (j + 1 >= m) break;
             const double h = R.h(j);
-            const Cubic qs = make_cubic(yl, yv[u], Ml, Mv[u], h), qP = make_cubic(Pl, Pv[u], MPl, MPv[u], h);
+            const Cubic qs = make_cubic(yl, yv[u], Ml, Mr, h), qP = make_cubic(Pl, Pv[u], MPl, MPr, h);
             walk_segment(W, qs, yv[u], qP, j == 0);
-            yl = yv[u], Pl = Pv[u], Ml = Mv[u], MPl = MPv[u];
+            yl = yv[u], Pl = Pv[u];
+            // advance: (M_j, M_{j+1}, M_{j+2}) -> (M_{j+1}, M_{j+2}, M_{j+3})
+            Ml = Mr, MPl = MPr, Mr = Mn, MPr = MPn;
+            if (j + 3 <= m - 2) {
+                Mn = gv[u] - ev[u] * Mr;
+                MPn = gPv[u] - ev[u] * MPr;
+            } else if (j + 3 == m - 1) {  // not-a-knot end: M_{m-1} from M_{m-2}, M_{m-3}
+                Mn = (1.0 + q1) * Mr - q1 * Ml;
+                MPn = (1.0 + q1) * MPr - q1 * MPl;
+            }
         }
     }
 }

@@ -241,8 +241,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
     if constexpr (DEPO == kDepoSamples) {
         if (r.steps == 0) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
             a.smp_psi[i] = psi_a;
-            a.smp_dpds[i] = 0.0;
-            a.smp_s[i] = a.s0 ? a.s0[i] : 0.0;
+            a.smp_dpds[i] = 0.0;  // arc lengths are implicit: s_k = s0 + k ds (FitArgs::S)
         }
     }
     const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
@@ -305,7 +304,6 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
             psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
         if constexpr (DEPO == kDepoSamples) {
             a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
-            a.smp_s[(size_t)r.steps * a.n + i] = (a.s0 ? a.s0[i] : 0.0) + r.steps * a.ds;
         }
         if constexpr (DEPO == kDepoBinned) {
             r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
@@ -833,7 +831,7 @@ __global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
 // ---------------------------------------------------------------------------
 // Reference-faithful deposition (torj_fitdepo.hpp): one lane per ray
 // ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(64) k_fit_depo(FitArgs a) {
+__global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
     const int m = a.steps[i] + 2;  // launch point, entry point, one per step
@@ -844,21 +842,37 @@ __global__ void __launch_bounds__(64) k_fit_depo(FitArgs a) {
     }
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
     RayData R{&a, i, m, a.s0[i], psi_at(a.coef, a.g, xl)};
-    nak_solve(R);
+    nak_eliminate(R);
     Walker W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
     walk_ray(W, R);
+    W.flush_run();
+    // the walk's root counts and shell sums are no-return atomics: wait for them
+    // before this lane reads its own counts back
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // the reference's outside-in walk stops at the first shell whose two
     // boundaries have < 2 roots together (src/plasma.jl:120-124)
+    // root counts: cnt[k] = sum_{j <= k} cdiff[j] = -sum_{j > k} cdiff[j] (the
+    // differences sum to zero), accumulated from the top
     int kstar = -1;
     const size_t n = a.n;
-    for (int k0 = a.n_psi - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
-        int cv[kChunk + 1];
+    const int L = a.n_psi;
+    int suf = a.cnt[(size_t)L * n + i];  // sum_{j > L-1} cdiff[j]
+    int c_up = -suf;                      // cnt[L-1]
+    for (int k0 = L - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
+        int dv[kChunk];
 #pragma unroll
-        for (int u = 0; u <= kChunk; u++) cv[u] = a.cnt[(size_t)max(k0 - u + 1, 0) * n + i];
+        for (int u = 0; u < kChunk; u++) dv[u] = a.cnt[(size_t)max(k0 - u + 1, 0) * n + i];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {  // shell k = k0 - u: boundaries k and k + 1
             const int k = k0 - u;
-            if (k >= 0 && kstar < 0 && cv[u + 1] + cv[u] < 2) kstar = k;
+            if (k >= 0 && kstar < 0) {
+                suf += dv[u];  // now sum_{j > k}
+                const int c_k = -suf;
+                if (c_up + c_k < 2) kstar = k;
+                c_up = c_k;
+            }
         }
     }
     a.kstar[i] = kstar;
@@ -1838,21 +1852,21 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         // per-boundary root counts, per-shell open-root integrals
         const size_t K = (size_t)cfg->n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
         const size_t b_smp = 3 * K * N * sizeof(double), b_m = 3 * K * N * sizeof(double);
-        const size_t b_cnt = (L * N + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
+        const size_t b_cnt = ((L + 1) * N * sizeof(int) + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
         const size_t b_ks = (N * sizeof(int) + 255) & ~(size_t)255;
         if (ensure_fit(p, b_smp + b_m + b_cnt + 2 * b_fo + b_ks)) return -1;
         char *base = (char *)p->d_fit;
         a.smp_psi = (double *)base;
         a.smp_dpds = a.smp_psi + K * N;
         a.smp_s = a.smp_dpds + K * N;
-        fa.cp = (double *)(base + b_smp);
-        fa.Mpsi = fa.cp + K * N;
-        fa.MP = fa.Mpsi + K * N;
-        fa.cnt = (unsigned char *)(base + b_smp + b_m);
+        fa.E = (double *)(base + b_smp);
+        fa.Gpsi = fa.E + K * N;
+        fa.GP = fa.Gpsi + K * N;
+        fa.cnt = (int *)(base + b_smp + b_m);
         fa.Fopen = (double *)(base + b_smp + b_m + b_cnt);
         fa.dPs = fa.Fopen + L * N;
         fa.kstar = (int *)(base + b_smp + b_m + b_cnt + 2 * b_fo);
-        HIPCK(hipMemsetAsync(fa.cnt, 0, L * N, s));
+        HIPCK(hipMemsetAsync(fa.cnt, 0, (L + 1) * N * sizeof(int), s));
         HIPCK(hipMemsetAsync(fa.Fopen, 0xFF, b_fo, s));  // NaN: every shell closed
         HIPCK(hipMemsetAsync(fa.dPs, 0, b_fo, s));
         fa.coef = p->d_coef;
@@ -1868,6 +1882,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         fa.smp_psi = a.smp_psi;
         fa.smp_dpds = a.smp_dpds;
         fa.smp_s = a.smp_s;
+        fa.s_uniform = cfg->integrator == 0;  // RK4: s_k = s0 + k ds, not stored
         fa.dP = dP;
         fa.Pray = Pdep;
         // uniform boundaries (np.linspace) get a direct index guess, checked
