@@ -3,8 +3,11 @@
 // functions and alpha of the device code against scipy / oracle/warm_ref.py
 // without a GPU.  Test harness only; the product calls these on the device.
 #include "torj_warm.hpp"
+#include "torj_fitdepo.hpp"
 
+#include <cmath>
 #include <mutex>
+#include <vector>
 
 extern "C" {
 void wh_zetac(int n, const double *x, const double *y, double *out) {
@@ -55,5 +58,51 @@ void wh_albajar(int n, const double *om, const double *X, const double *Y, const
     });
     for (int i = 0; i < n; i++)
         alpha[i] = torj::abs_albajar_fast(g_wh_gl, om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], mode, nullptr);
+}
+
+// power_deposition_profile of the product (torj_fitdepo.hpp fit_depo_ray, the
+// body of k_fit_depo) on the host, one call per ray, with an open-shell cache
+// of nc = 1, 2 or 4 entries (1 exercises the spill path).  Samples are the
+// oracle's (psi_k, dP/ds_k) at the entry point and each RK4 step, (n_steps+1) x n;
+// outputs: dPs (n_psi-1) x n shell powers before the break, kstar, P per ray.
+void fd_profile(int n, int n_steps, int n_psi, double ds, const double *grid, const double *s0,
+                const int *steps, const double *psiL, const double *smp_psi, const double *smp_dpds,
+                int nc, double *dPs, int *kstar, double *Pray) {
+    const size_t K = (size_t)n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
+    std::vector<double> E(K * N), G1(K * N), G2(K * N), Fo(L * N, NAN), dp(L * N, 0.0);
+    std::vector<int> cnt((L + 1) * N, 0);
+    torj::FitArgs fa{};
+    fa.n = n;
+    fa.n_psi = n_psi;
+    fa.ds = ds;
+    fa.grid = grid;
+    const double dg = (grid[n_psi - 1] - grid[0]) / (n_psi - 1);
+    bool uni = dg > 0;
+    for (int k = 0; uni && k < n_psi; k++) uni = std::fabs(grid[k] - (grid[0] + k * dg)) <= 1e-9 * dg;
+    fa.uniform = uni;
+    fa.g0 = grid[0];
+    fa.ginv = uni ? 1.0 / dg : 0.0;
+    fa.s0 = s0;
+    fa.steps = steps;
+    fa.smp_psi = smp_psi;
+    fa.smp_dpds = smp_dpds;
+    fa.smp_s = nullptr;
+    fa.s_uniform = 1;
+    fa.E = E.data(), fa.Gpsi = G1.data(), fa.GP = G2.data();
+    fa.cnt = cnt.data();
+    fa.Fopen = Fo.data();
+    fa.dPs = dp.data();
+    fa.kstar = kstar;
+    fa.Pray = Pray;
+    for (int i = 0; i < n; i++) {
+        if (nc == 1)
+            torj::fit_depo_ray<1>(fa, i, psiL[i]);
+        else if (nc == 4)
+            torj::fit_depo_ray<4>(fa, i, psiL[i]);
+        else
+            torj::fit_depo_ray<2>(fa, i, psiL[i]);
+    }
+    for (size_t k = 0; k + 1 < L; k++)
+        for (size_t i = 0; i < N; i++) dPs[k * N + i] = dp[k * N + i];
 }
 }

@@ -54,6 +54,9 @@ struct FitArgs {
     double *Pray;                      // n: per-ray deposited power (reference's P)
 };
 
+TORJ_HD int imin(int x, int y) { return x < y ? x : y; }
+TORJ_HD int imax(int x, int y) { return x > y ? x : y; }
+
 constexpr int kChunk = 8;      // points per prefetch batch of the sequential sweeps
 constexpr int kWalkChunk = 4;  // the walk's batch (five streams, the heavy segment code)
 
@@ -63,16 +66,16 @@ struct RayData {
     double s0, psiL;
     // arc length of point j: 0 (launch), s0 (entry), s0 + (j-1) ds for RK4 (the
     // fma the trajectory output uses), else the integrator's stored s
-    __device__ double S(int j) const {
+    TORJ_HD double S(int j) const {
         if (j == 0) return 0.0;
         return a->s_uniform ? fma((double)(j - 1), a->ds, s0) : a->smp_s[(size_t)(j - 1) * a->n + i];
     }
-    __device__ double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
-    __device__ double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[(size_t)(j - 1) * a->n + i]; }
-    __device__ double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[(size_t)(j - 1) * a->n + i]; }
-    __device__ double &EE(int j) const { return a->E[(size_t)j * a->n + i]; }
-    __device__ double &GPSI(int j) const { return a->Gpsi[(size_t)j * a->n + i]; }
-    __device__ double &GPP(int j) const { return a->GP[(size_t)j * a->n + i]; }
+    TORJ_HD double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
+    TORJ_HD double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[(size_t)(j - 1) * a->n + i]; }
+    TORJ_HD double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[(size_t)(j - 1) * a->n + i]; }
+    TORJ_HD double &EE(int j) const { return a->E[(size_t)j * a->n + i]; }
+    TORJ_HD double &GPSI(int j) const { return a->Gpsi[(size_t)j * a->n + i]; }
+    TORJ_HD double &GPP(int j) const { return a->GP[(size_t)j * a->n + i]; }
 };
 
 // not-a-knot cubic interpolation of psi and dP/ds (m >= 4 points): second
@@ -82,7 +85,7 @@ struct RayData {
 // bottom up (this sweep stores e_r, g_r with M_r = g_r - e_r M_{r-1}), so the
 // substitution runs upwards in s and fuses with the root walk (walk_ray): one
 // stored sweep instead of two.
-__device__ __forceinline__ void nak_eliminate(const RayData &R) {
+TORJ_HD void nak_eliminate(const RayData &R) {
     const int m = R.m;
     const double h0 = R.h(0), h1 = R.h(1), hm2 = R.h(m - 2), hm3 = R.h(m - 3);
     double yn = R.Ypsi(m - 1), yc = R.Ypsi(m - 2), Pn = R.YP(m - 1), Pc = R.YP(m - 2);
@@ -92,7 +95,7 @@ __device__ __forceinline__ void nak_eliminate(const RayData &R) {
         double yv[kChunk], Pv[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
-            const int j = max(r0 - 1 - u, 0);
+            const int j = imax(r0 - 1 - u, 0);
             yv[u] = R.Ypsi(j);
             Pv[u] = R.YP(j);
         }
@@ -129,14 +132,14 @@ __device__ __forceinline__ void nak_eliminate(const RayData &R) {
 
 struct Cubic {  // y0 + t (b + t (c + t d)), t in [0, h]
     double y0, b, c, d, h;
-    __device__ double f(double t) const { return fma(t, fma(t, fma(t, d, c), b), y0); }
-    __device__ double df(double t) const { return fma(t, fma(t, 3.0 * d, 2.0 * c), b); }
-    __device__ double G(double t) const {  // integral 0..t
+    TORJ_HD double f(double t) const { return fma(t, fma(t, fma(t, d, c), b), y0); }
+    TORJ_HD double df(double t) const { return fma(t, fma(t, 3.0 * d, 2.0 * c), b); }
+    TORJ_HD double G(double t) const {  // integral 0..t
         return t * fma(t, fma(t, fma(t, 0.25 * d, c * (1.0 / 3.0)), 0.5 * b), y0);
     }
 };
 
-__device__ Cubic make_cubic(double y0, double y1, double M0, double M1, double h) {
+TORJ_HD Cubic make_cubic(double y0, double y1, double M0, double M1, double h) {
     Cubic q;
     q.y0 = y0;
     q.h = h;
@@ -147,7 +150,7 @@ __device__ Cubic make_cubic(double y0, double y1, double M0, double M1, double h
 }
 
 // smallest boundary index k with grid[k] > x (strict) / >= x
-__device__ int level_above(const FitArgs &a, double x, bool strict) {
+TORJ_HD int level_above(const FitArgs &a, double x, bool strict) {
     int k;
     if (a.uniform) {
         const double u = (x - a.g0) * a.ginv;
@@ -175,11 +178,11 @@ struct Cursor {
     const FitArgs *a;
     int c;
     double lo, hi;  // grid[c-1] (or -inf), grid[c] (or +inf)
-    __device__ __forceinline__ void load() {
+    TORJ_HD void load() {
         lo = c > 0 ? a->grid[c - 1] : -INFINITY;
         hi = c < a->n_psi ? a->grid[c] : INFINITY;
     }
-    __device__ __forceinline__ void seek(double v) {  // c = #boundaries <= v
+    TORJ_HD void seek(double v) {  // c = #boundaries <= v
         if (v >= lo && v < hi) return;
         while (c < a->n_psi && a->grid[c] <= v) c++;
         while (c > 0 && a->grid[c - 1] > v) c--;
@@ -189,7 +192,7 @@ struct Cursor {
 
 // root of the monotone cubic piece q(t) = L on [ta, tb], L strictly between
 // the end values: Newton with a bisection safeguard, to the last bit
-__device__ double cubic_root(const Cubic &q, double L, double ta, double tb, bool up) {
+TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, bool up) {
     double lo = ta, hi = tb, t = 0.5 * (ta + tb);
     for (int it = 0; it < 100; it++) {
         const double v = q.f(t) - L;
@@ -221,32 +224,33 @@ __device__ double cubic_root(const Cubic &q, double L, double ta, double tb, boo
 #endif
 constexpr int kOpenCache = 2;
 
+template <int NC = kOpenCache>
 struct Walker {
     const FitArgs *a;
     int i;
     double Fhi, Flo;  // compensated running integral of dP/ds at the segment start
     Cursor cur;
-    int oq[kOpenCache];     // open shell ids (-1: free slot)
-    double oF[kOpenCache];  // F at their opening root
+    int oq[NC];     // open shell ids (-1: free slot)
+    double oF[NC];  // F at their opening root
     bool spilled;           // some open shell lives in Fopen
     int run_k0, run_k1, run_d;  // current run of roots (run_d = 0: none)
-    __device__ __forceinline__ void init() {
+    TORJ_HD void init() {
 #pragma unroll
-        for (int u = 0; u < kOpenCache; u++) oq[u] = -1, oF[u] = 0.0;
+        for (int u = 0; u < NC; u++) oq[u] = -1, oF[u] = 0.0;
         spilled = false;
         run_d = 0, run_k0 = run_k1 = 0;
     }
-    __device__ __forceinline__ void cadd(int k, int v) {
+    TORJ_HD void cadd(int k, int v) {
         __hip_atomic_fetch_add(a->cnt + (size_t)k * a->n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    __device__ __forceinline__ void flush_run() {
+    TORJ_HD void flush_run() {
         if (run_d == 0) return;
         const int lo = run_k0 < run_k1 ? run_k0 : run_k1, hi = run_k0 < run_k1 ? run_k1 : run_k0;
         cadd(lo, 1);
         cadd(hi + 1, -1);
         run_d = 0;
     }
-    __device__ __forceinline__ void close(int q, double d) {  // |integrate(dP_ds, r1, r2)|
+    TORJ_HD void close(int q, double d) {  // |integrate(dP_ds, r1, r2)|
         double *p = a->dPs + (size_t)q * a->n + i;
 #if TORJ_DEPO_ATOMIC
         __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -254,11 +258,11 @@ struct Walker {
         *p += d;
 #endif
     }
-    __device__ __forceinline__ void toggle(int q, double Fr) {
+    TORJ_HD void toggle(int q, double Fr) {
         bool hit = false;
         double fo = 0.0;
 #pragma unroll
-        for (int u = 0; u < kOpenCache; u++)
+        for (int u = 0; u < NC; u++)
             if (!hit && oq[u] == q) hit = true, fo = oF[u], oq[u] = -1;
         if (!hit && spilled) {  // maybe open in memory
             double &m = a->Fopen[(size_t)q * a->n + i];
@@ -271,7 +275,7 @@ struct Walker {
         }
         bool placed = false;
 #pragma unroll
-        for (int u = 0; u < kOpenCache; u++)
+        for (int u = 0; u < NC; u++)
             if (!placed && oq[u] < 0) placed = true, oq[u] = q, oF[u] = Fr;
         if (!placed) {  // spill slot 0 (rare: > 2 shells open at once)
             a->Fopen[(size_t)oq[0] * a->n + i] = oF[0];
@@ -282,7 +286,7 @@ struct Walker {
     // a root of boundary L_k at running integral Fr, found while the boundary
     // levels are crossed in direction d (+1 upwards, -1 downwards): count it and
     // toggle the shells it bounds (k-1 above it, k below it)
-    __device__ __forceinline__ void root(int k, double Fr, int d) {
+    TORJ_HD void root(int k, double Fr, int d) {
         if (d == run_d && k == run_k1 + d) {
             run_k1 = k;
         } else {
@@ -300,7 +304,8 @@ struct Walker {
 // The segment splits at the zeros of psi' into at most three monotone pieces
 // [0, c1], [c1, c2], [c2, h] (absent cuts sit at h and give empty pieces); one
 // rolled piece loop and one root loop keep the code (and registers) small.
-__device__ __forceinline__ void walk_segment(Walker &W, const Cubic &qs, double y1, const Cubic &qP, bool first) {
+template <class W_>
+TORJ_HD void walk_segment(W_ &W, const Cubic &qs, double y1, const Cubic &qP, bool first) {
     const FitArgs &a = *W.a;
     const double A = 3.0 * qs.d, B = 2.0 * qs.c, C = qs.b;
     const double disc = B * B - 4.0 * A * C;
@@ -369,7 +374,8 @@ __device__ __forceinline__ void walk_segment(Walker &W, const Cubic &qs, double 
 
 // the root walk over the segments, with the spline's second derivatives from
 // the upward substitution M_r = g_r - e_r M_{r-1} (nak_eliminate) as it goes
-__device__ __forceinline__ void walk_ray(Walker &W, const RayData &R) {
+template <class W_>
+TORJ_HD void walk_ray(W_ &W, const RayData &R) {
     const int m = R.m;
     const double q0 = R.h(0) / R.h(1), q1 = R.h(m - 2) / R.h(m - 3);
     const double M1 = R.GPSI(1), M1P = R.GPP(1);
@@ -384,10 +390,10 @@ __device__ __forceinline__ void walk_ray(Walker &W, const RayData &R) {
         double yv[kWalkChunk], Pv[kWalkChunk], ev[kWalkChunk], gv[kWalkChunk], gPv[kWalkChunk];
 #pragma unroll
         for (int u = 0; u < kWalkChunk; u++) {
-            const int j = min(j0 + 1 + u, m - 1);
+            const int j = imin(j0 + 1 + u, m - 1);
             yv[u] = R.Ypsi(j);
             Pv[u] = R.YP(j);
-            const int r = min(j0 + 3 + u, m - 2);  // row of M_{j+3}, prepared after segment j+1
+            const int r = imin(j0 + 3 + u, m - 2);  // row of M_{j+3}, prepared after segment j+1
             ev[u] = R.EE(r);
             gv[u] = R.GPSI(r);
             gPv[u] = R.GPP(r);
@@ -411,6 +417,67 @@ __device__ __forceinline__ void walk_ray(Walker &W, const RayData &R) {
             }
         }
     }
+}
+
+
+// One ray of power_deposition_profile (k_fit_depo; the CPU suite runs the host
+// build through tests/native): spline fits, the root walk, the outside-in break
+// shell k* and the ray's deposited power P.  psiL = psi at the launch point.
+template <int NC>
+TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
+    const int m = a.steps[i] + 2;  // launch point, entry point, one per step
+    if (m < 4 || !(a.s0[i] > 0.0)) {  // FITPACK needs > k = 3 strictly increasing points
+        a.kstar[i] = a.n_psi;  // no shell counts
+        a.Pray[i] = 0.0;
+        return;
+    }
+    RayData R{&a, i, m, a.s0[i], psiL};
+    nak_eliminate(R);
+    Walker<NC> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
+    walk_ray(W, R);
+    W.flush_run();
+    // the walk's root counts and shell sums are no-return atomics: wait for them
+    // before this lane reads its own counts back
+#ifdef __HIP_DEVICE_COMPILE__
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    // the reference's outside-in walk stops at the first shell whose two
+    // boundaries have < 2 roots together (src/plasma.jl:120-124)
+    // root counts: cnt[k] = sum_{j <= k} cdiff[j] = -sum_{j > k} cdiff[j] (the
+    // differences sum to zero), accumulated from the top
+    int kstar = -1;
+    const size_t n = a.n;
+    const int L = a.n_psi;
+    int suf = a.cnt[(size_t)L * n + i];  // sum_{j > L-1} cdiff[j]
+    int c_up = -suf;                      // cnt[L-1]
+    for (int k0 = L - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
+        int dv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) dv[u] = a.cnt[(size_t)imax(k0 - u + 1, 0) * n + i];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) {  // shell k = k0 - u: boundaries k and k + 1
+            const int k = k0 - u;
+            if (k >= 0 && kstar < 0) {
+                suf += dv[u];  // now sum_{j > k}
+                const int c_k = -suf;
+                if (c_up + c_k < 2) kstar = k;
+                c_up = c_k;
+            }
+        }
+    }
+    a.kstar[i] = kstar;
+    double P = 0.0;
+    for (int q0 = a.n_psi - 2; q0 > kstar; q0 -= kChunk) {
+        double v[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++) v[u] = a.dPs[(size_t)imax(q0 - u, 0) * n + i];
+#pragma unroll
+        for (int u = 0; u < kChunk; u++)
+            if (q0 - u > kstar) P += v[u];
+    }
+    a.Pray[i] = P;
 }
 
 }  // namespace torj

@@ -834,63 +834,9 @@ __global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
 __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
-    const int m = a.steps[i] + 2;  // launch point, entry point, one per step
-    if (m < 4 || !(a.s0[i] > 0.0)) {  // FITPACK needs > k = 3 strictly increasing points
-        a.kstar[i] = a.n_psi;  // no shell counts
-        a.Pray[i] = 0.0;
-        return;
-    }
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
-    RayData R{&a, i, m, a.s0[i], psi_at(a.coef, a.g, xl)};
-    nak_eliminate(R);
-    Walker W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
-    W.init();
-    walk_ray(W, R);
-    W.flush_run();
-    // the walk's root counts and shell sums are no-return atomics: wait for them
-    // before this lane reads its own counts back
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    // the reference's outside-in walk stops at the first shell whose two
-    // boundaries have < 2 roots together (src/plasma.jl:120-124)
-    // root counts: cnt[k] = sum_{j <= k} cdiff[j] = -sum_{j > k} cdiff[j] (the
-    // differences sum to zero), accumulated from the top
-    int kstar = -1;
-    const size_t n = a.n;
-    const int L = a.n_psi;
-    int suf = a.cnt[(size_t)L * n + i];  // sum_{j > L-1} cdiff[j]
-    int c_up = -suf;                      // cnt[L-1]
-    for (int k0 = L - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
-        int dv[kChunk];
-#pragma unroll
-        for (int u = 0; u < kChunk; u++) dv[u] = a.cnt[(size_t)max(k0 - u + 1, 0) * n + i];
-#pragma unroll
-        for (int u = 0; u < kChunk; u++) {  // shell k = k0 - u: boundaries k and k + 1
-            const int k = k0 - u;
-            if (k >= 0 && kstar < 0) {
-                suf += dv[u];  // now sum_{j > k}
-                const int c_k = -suf;
-                if (c_up + c_k < 2) kstar = k;
-                c_up = c_k;
-            }
-        }
-    }
-    a.kstar[i] = kstar;
-    double P = 0.0;
-    for (int q0 = a.n_psi - 2; q0 > kstar; q0 -= kChunk) {
-        double v[kChunk];
-#pragma unroll
-        for (int u = 0; u < kChunk; u++) v[u] = a.dPs[(size_t)max(q0 - u, 0) * n + i];
-#pragma unroll
-        for (int u = 0; u < kChunk; u++)
-            if (q0 - u > kstar) P += v[u];
-    }
-    a.Pray[i] = P;
+    fit_depo_ray<kOpenCache>(a, i, psi_at(a.coef, a.g, xl));
 }
-
-// make_beam's sums over rays (src/solve.jl:236-239), atomic-free per shell:
-// dP[k] += sum_i w_i dP_k(ray i) over rays whose outside-in walk reached k;
-// block n_psi - 1 sums w_i P_i into dP[n_psi].
 __global__ void __launch_bounds__(256) k_shell_sum(FitArgs a) {
     const int k = blockIdx.x;
     double acc = 0.0;
