@@ -57,57 +57,135 @@ constexpr int kWarmMaxL = 5;  // i_max (src/constants.jl:4)
 constexpr int kNtv = 501;     // t-quadrature (src/constants.jl:1-3)
 constexpr double kTmax = 5.0, kDtv = 2.0 * kTmax / (kNtv - 1);
 
-// exp(-x) Ei(x) (calcei int = 3, :29-232), restated: power series of Ei / E1
-// near 0, continued fraction for e^y E1(y) (y > 1), asymptotic series for
-// |x| >= 40.  -1.79e308 at x = 0 (the reference's -xinf).
+// exp(-x) Ei(x) (expei, :29-232): W. J. Cody's CALCEI (int = 3), the
+// algorithm the reference transliterates -- fixed-cost rational
+// approximations per interval (Cody & Thacher, Math. Comp. 22 (1968) and 23
+// (1969); SPECFUN), with their published coefficients:
+//   x < 0:       y = -x: y <= 1  (ln y - P6(y)/Q6(y)) e^y,
+//                        y <= 4  -P8(1/y)/Q8(1/y),
+//                        y > 4   w (w P9(w)/Q9(w) - 1), w = 1/y;
+//   0 < x < 6:   Chebyshev-form ratio in t = 2x/3 - 2, with ln(x/x0) near the
+//                zero x0 of Ei;
+//   6 <= x < 24: J-fractions; x >= 24: J-fraction in 1/x.
+// -1.79e308 at x = 0 (the reference's -xinf).
+namespace cody {
+constexpr double A[7] = {1.1669552669734461083368e2, 2.1500672908092918123209e3, 1.5924175980637303639884e4,
+                         8.9904972007457256553251e4, 1.5026059476436982420737e5, -1.4815102102575750838086e5,
+                         5.0196785185439843791020e0};
+constexpr double B[6] = {4.0205465640027706061433e1, 7.5043163907103936624165e2, 8.1258035174768735759855e3,
+                         5.2440529172056355429883e4, 1.8434070063353677359298e5, 2.5666493484897117319268e5};
+constexpr double C[9] = {3.828573121022477169108e-1, 1.107326627786831743809e+1, 7.246689782858597021199e+1,
+                         1.700632978311516129328e+2, 1.698106763764238382705e+2, 7.633628843705946890896e+1,
+                         1.487967702840464066613e+1, 9.999989642347613068437e-1, 1.737331760720576030932e-8};
+constexpr double D[9] = {8.258160008564488034698e-2, 4.344836335509282083360e+0, 4.662179610356861756812e+1,
+                         1.775728186717289799677e+2, 2.953136335677908517423e+2, 2.342573504717625153053e+2,
+                         9.021658450529372642314e+1, 1.587964570758947927903e+1, 1.0};
+constexpr double E[10] = {1.3276881505637444622987e+2, 3.5846198743996904308695e+4, 1.7283375773777593926828e+5,
+                          2.6181454937205639647381e+5, 1.7503273087497081314708e+5, 5.9346841538837119172356e+4,
+                          1.0816852399095915622498e+4, 1.0611777263550331766871e+3, 5.2199632588522572481039e+1,
+                          9.9999999999999999087819e-1};
+constexpr double F[10] = {3.9147856245556345627078e+4, 2.5989762083608489777411e+5, 5.5903756210022864003380e+5,
+                          5.4616842050691155735758e+5, 2.7858134710520842139357e+5, 7.9231787945279043698718e+4,
+                          1.2842808586627297365998e+4, 1.1635769915320848035459e+3, 5.4199632588522559414924e+1,
+                          1.0};
+constexpr double PLG[4] = {-2.4562334077563243311e+01, 2.3642701335621505212e+02, -5.4989956895857911039e+02,
+                           3.5687548468071500413e+02};
+constexpr double QLG[4] = {-3.5553900764052419184e+01, 1.9400230218539473193e+02, -3.3442903192607538956e+02,
+                           1.7843774234035750207e+02};
+constexpr double P[10] = {-1.2963702602474830028590e+01, -1.2831220659262000678155e+03, -1.4287072500197005777376e+04,
+                          -1.4299841572091610380064e+06, -3.1398660864247265862050e+05, -3.5377809694431133484800e+08,
+                          3.1984354235237738511048e+08, -2.5301823984599019348858e+10, 1.2177698136199594677580e+10,
+                          -2.0829040666802497120940e+11};
+constexpr double Q[10] = {7.6886718750000000000000e+01, -5.5648470543369082846819e+03, 1.9418469440759880361415e+05,
+                          -4.2648434812177161405483e+06, 6.4698830956576428587653e+07, -7.0108568774215954065376e+08,
+                          5.4229617984472955011862e+09, -2.8986272696554495342658e+10, 9.8900934262481749439886e+10,
+                          -8.9673749185755048616855e+10};
+constexpr double R[10] = {-2.645677793077147237806e+00, -2.378372882815725244124e+00, -2.421106956980653511550e+01,
+                          1.052976392459015155422e+01, 1.945603779539281810439e+01, -3.015761863840593359165e+01,
+                          1.120011024227297451523e+01, -3.988850730390541057912e+00, 9.565134591978630774217e+00,
+                          9.981193787537396413219e-1};
+constexpr double S[9] = {1.598517957704779356479e-4, 4.644185932583286942650e+00, 3.697412299772985940785e+02,
+                         -8.791401054875438925029e+00, 7.608194509086645763123e+02, 2.852397548119248700147e+01,
+                         4.731097187816050252967e+02, -2.369210235636181001661e+02, 1.249884822712447891440e+00};
+constexpr double P1[10] = {-1.647721172463463140042e+00, -1.860092121726437582253e+01, -1.000641913989284829961e+01,
+                           -2.105740799548040450394e+01, -9.134835699998742552432e-1, -3.323612579343962284333e+01,
+                           2.495487730402059440626e+01, 2.652575818452799819855e+01, -1.845086232391278674524e+00,
+                           9.999933106160568739091e-1};
+constexpr double Q1[9] = {9.792403599217290296840e+01, 6.403800405352415551324e+01, 5.994932325667407355255e+01,
+                          2.538819315630708031713e+02, 4.429413178337928401161e+01, 1.192832423968601006985e+03,
+                          1.991004470817742470726e+02, -1.093556195391091143924e+01, 1.001533852045342697818e+00};
+constexpr double P2[10] = {1.75338801265465972390e+02, -2.23127670777632409550e+02, -1.81949664929868906455e+01,
+                           -2.79798528624305389340e+01, -7.63147701620253630855e+00, -1.52856623636929636839e+01,
+                           -7.06810977895029358836e+00, -5.00006640413131002475e+00, -3.00000000320981265753e+00,
+                           1.00000000000000485503e+00};
+constexpr double Q2[9] = {3.97845977167414720840e+04, 3.97277109100414518365e+00, 1.37790390235747998793e+02,
+                          1.17179220502086455287e+02, 7.04831847180424675988e+01, -1.20187763547154743238e+01,
+                          -7.99243595776339741065e+00, -2.99999894040324959612e+00, 1.99999999999048104167e+00};
+constexpr double kX0 = 0.37250741078136663466;  // zero of Ei
+constexpr double kX01 = 381.5, kX11 = 1024.0, kX02 = -5.1182968633365538008e-5;
+
+// P(u) / Q(u) with leading coefficients first (Horner), N terms each
+template <int NP, int NQ>
+TORJ_HD double ratio(const double (&p)[NP], const double (&q)[NQ], double u) {
+    double sp = p[0], sq = q[0];
+#pragma unroll
+    for (int i = 1; i < NP; i++) sp = fma(sp, u, p[i]);
+#pragma unroll
+    for (int i = 1; i < NQ; i++) sq = fma(sq, u, q[i]);
+    return sp / sq;
+}
+
+// J-fraction s1/(r1 + x + s2/(r2 + x + ...)), evaluated from the innermost term
+template <int N>
+TORJ_HD double jfrac(const double (&r)[N + 1], const double (&s)[N], double x) {
+    double f = 0.0;
+#pragma unroll
+    for (int i = 0; i < N; i++) f = s[i] / (r[i] + x + f);
+    return f;
+}
+}  // namespace cody
+
 TORJ_HD double expei(double x) {
     if (x == 0.0) return -1.79e308;
-    const double ax = fabs(x);
-    if (ax >= 40.0) {  // e^-x Ei(x) ~ (1/x) sum_k k!/x^k (both signs)
-        double s = 1.0, term = 1.0;
-        for (int k = 1; k < 40; k++) {
-            const double nt = term * k / x;
-            if (fabs(nt) >= fabs(term)) break;  // optimal truncation
-            term = nt;
-            s += term;
-            if (fabs(term) < 1e-17 * fabs(s)) break;
-        }
-        return s / x;
-    }
     if (x < 0.0) {
         const double y = -x;
-        if (y <= 1.0) {  // E1(y) = -gamma - ln y - sum (-y)^k / (k k!)
-            double s = 0.0, term = 1.0;
-            for (int k = 1; k <= 24; k++) {
-                term *= -y / k;
-                s += term / k;
+        if (y <= 1.0) {  // the y <= 1 numerator is stored in the reference's order: its last term leads
+            double sp = fma(cody::A[6], y, cody::A[0]), sq = y + cody::B[0];
+#pragma unroll
+            for (int i = 1; i < 6; i++) {
+                sp = fma(sp, y, cody::A[i]);
+                sq = fma(sq, y, cody::B[i]);
             }
-            const double E1 = -kEulerGamma - log(y) - s;
-            return -exp(y) * E1;
+            return (log(y) - sp / sq) * exp(y);
         }
-        // e^y E1(y) = 1 / (y + 1 - 1 / (y + 3 - 4 / (y + 5 - ...))), modified Lentz
-        const double tiny = 1e-300;
-        double b = y + 1.0, c = 1.0 / tiny, d = 1.0 / b, h = d;
-        for (int k = 1; k < 300; k++) {
-            const double an = -(double)k * k;
-            b += 2.0;
-            d = 1.0 / (an * d + b);
-            c = b + an / c;
-            const double del = c * d;
-            h *= del;
-            if (fabs(del - 1.0) < 1e-16) break;
+        const double w = 1.0 / y;
+        if (y <= 4.0) return -cody::ratio(cody::C, cody::D, w);
+        return w * (w * cody::ratio(cody::E, cody::F, w) - 1.0);
+    }
+    if (x < 6.0) {  // Chebyshev-form ratio in t (Clenshaw-like three-term recurrence)
+        const double t = (x + x) / 3.0 - 2.0;
+        double pm1 = 0.0, qm1 = 0.0, pc = cody::P[0], qc = cody::Q[0];
+#pragma unroll
+        for (int i = 1; i < 9; i++) {
+            const double pn = t * pc - pm1 + cody::P[i], qn = t * qc - qm1 + cody::Q[i];
+            pm1 = pc, qm1 = qc, pc = pn, qc = qn;
         }
-        return -h;  // e^-x Ei(x) = -e^y E1(y)
+        const double frac = (0.5 * t * pc - pm1 + cody::P[9]) / (0.5 * t * qc - qm1 + cody::Q[9]);
+        const double xmx0 = (x - cody::kX01 / cody::kX11) - cody::kX02;
+        if (fabs(xmx0) >= 0.037) return exp(-x) * (log(x / cody::kX0) + xmx0 * frac);
+        const double yy = xmx0 / (x + cody::kX0), ysq = yy * yy;  // ln(x/x0) near x0
+        double sp = cody::PLG[0], sq = ysq + cody::QLG[0];
+#pragma unroll
+        for (int i = 1; i < 4; i++) {
+            sp = fma(sp, ysq, cody::PLG[i]);
+            sq = fma(sq, ysq, cody::QLG[i]);
+        }
+        return exp(-x) * (sp / (sq * (x + cody::kX0)) + frac) * xmx0;
     }
-    // 0 < x < 40: Ei(x) = gamma + ln x + sum x^k / (k k!)
-    double s = 0.0, term = 1.0;
-    for (int k = 1; k < 200; k++) {
-        term *= x / k;
-        const double add = term / k;
-        s += add;
-        if (add < 1e-17 * s) break;
-    }
-    return exp(-x) * (kEulerGamma + log(x) + s);
+    if (x < 12.0) return (cody::R[9] + cody::jfrac<9>(cody::R, cody::S, x)) / x;
+    if (x <= 24.0) return (cody::P1[9] + cody::jfrac<9>(cody::P1, cody::Q1, x)) / x;
+    const double y = 1.0 / x;
+    return y + y * y * (cody::P2[9] + cody::jfrac<9>(cody::P2, cody::Q2, x));
 }
 
 TORJ_HD double factd(int k) {
