@@ -57,6 +57,40 @@ constexpr int kWarmMaxL = 5;  // i_max (src/constants.jl:4)
 constexpr int kNtv = 501;     // t-quadrature (src/constants.jl:1-3)
 constexpr double kTmax = 5.0, kDtv = 2.0 * kTmax / (kNtv - 1);
 
+// exp(x) in constant evaluation (x <= 0): x = k ln2 + r, |r| <= ln2/2, a
+// 24-term Taylor sum for e^r and an exact power-of-two scaling (~1 ulp)
+constexpr double cexp(double x) {
+    const double ln2hi = 6.93147180369123816490e-01, ln2lo = 1.90821492927058770002e-10;
+    const double kf = x / (ln2hi + ln2lo);
+    const long k = (long)(kf < 0 ? kf - 0.5 : kf + 0.5);
+    const double r = (x - k * ln2hi) - k * ln2lo;
+    double term = 1.0, sum = 1.0;
+    for (int i = 1; i < 24; i++) {
+        term *= r / i;
+        sum += term;
+    }
+    for (long j = 0; j < (k < 0 ? -k : k); j++) sum = k < 0 ? sum * 0.5 : sum * 2.0;
+    return sum;
+}
+// the quadrature weights exp(-t_i^2) dt of the fully relativistic hermitian
+// part (:646-950): t-only, so a compile-time table (scalar loads: i is uniform)
+struct FrWeights {
+    double w[kNtv];
+};
+constexpr FrWeights make_fr_weights() {
+    FrWeights f{};
+    for (int i = 0; i < kNtv; i++) {
+        const double t = -kTmax + i * kDtv;
+        f.w[i] = cexp(-t * t) * kDtv;
+    }
+    return f;
+}
+#ifdef __HIP_DEVICE_COMPILE__
+__constant__ constexpr FrWeights kFrW = make_fr_weights();
+#else
+constexpr FrWeights kFrW = make_fr_weights();
+#endif
+
 // exp(-x) Ei(x) (expei, :29-232): W. J. Cody's CALCEI (int = 3), the
 // algorithm the reference transliterates -- fixed-cost rational
 // approximations per interval (Cody & Thacher, Math. Comp. 22 (1968) and 23
@@ -475,15 +509,16 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
     const double cr = -amu * amu / (kSqrtPi * cmxw);
     const double bth2 = 2.0 / amu, bth = sqrt(bth2);
     const double amu2 = amu * amu, amu4 = amu2 * amu2, amu6 = amu4 * amu2;
+    const double iamu = 1.0 / amu, i2amu = 0.5 * iamu;
     for (int n = -llm; n <= llm; n++) {
         const int mlo = n < 0 ? -n : n;
         double acc[4][3];
         for (int m = 0; m < 4; m++) acc[m][0] = acc[m][1] = acc[m][2] = 0.0;
         for (int i = 0; i < kNtv; i++) {
-            const double t = -kTmax + i * kDtv;
-            const double rxt = sqrt(1.0 + t * t / (2.0 * amu)), x = t * rxt;
-            const double upl2 = bth2 * x * x, upl = bth * x, gx = 1.0 + t * t / amu;
-            const double exdx = cr * (exp(-t * t) * kDtv) * gx / rxt;
+            const double t = -kTmax + i * kDtv, t2 = t * t;
+            const double rxt = sqrt_pos(fma(t2, i2amu, 1.0)), x = t * rxt;
+            const double upl2 = bth2 * x * x, upl = bth * x, gx = fma(t2, iamu, 1.0);
+            const double exdx = cr * kFrW.w[i] * gx * rcp_nz(rxt);
             const double gr = anpl * upl + n * yg;
             const double zm = -amu * (gx - gr), s = amu * (gx + gr);
             const double fe0m = expei(zm), zm2 = zm * zm;
