@@ -166,7 +166,7 @@ TORJ_HD double ratio(const double (&p)[NP], const double (&q)[NQ], double u) {
     for (int i = 1; i < NP; i++) sp = fma(sp, u, p[i]);
 #pragma unroll
     for (int i = 1; i < NQ; i++) sq = fma(sq, u, q[i]);
-    return sp / sq;
+    return sp * rcp_nz(sq);  // Cody's denominators are positive on their intervals
 }
 
 // J-fraction s1/(r1 + x + s2/(r2 + x + ...)), evaluated from the innermost term
@@ -174,7 +174,7 @@ template <int N>
 TORJ_HD double jfrac(const double (&r)[N + 1], const double (&s)[N], double x) {
     double f = 0.0;
 #pragma unroll
-    for (int i = 0; i < N; i++) f = s[i] / (r[i] + x + f);
+    for (int i = 0; i < N; i++) f = s[i] * rcp_nz(r[i] + x + f);
     return f;
 }
 }  // namespace cody
@@ -192,7 +192,7 @@ TORJ_HD double expei(double x) {
             }
             return (log(y) - sp / sq) * exp(y);
         }
-        const double w = 1.0 / y;
+        const double w = rcp_nz(y);
         if (y <= 4.0) return -cody::ratio(cody::C, cody::D, w);
         return w * (w * cody::ratio(cody::E, cody::F, w) - 1.0);
     }
@@ -218,7 +218,7 @@ TORJ_HD double expei(double x) {
     }
     if (x < 12.0) return (cody::R[9] + cody::jfrac<9>(cody::R, cody::S, x)) / x;
     if (x <= 24.0) return (cody::P1[9] + cody::jfrac<9>(cody::P1, cody::Q1, x)) / x;
-    const double y = 1.0 / x;
+    const double y = rcp_nz(x);
     return y + y * y * (cody::P2[9] + cody::jfrac<9>(cody::P2, cody::Q2, x));
 }
 
