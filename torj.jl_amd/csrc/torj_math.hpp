@@ -107,6 +107,39 @@ TORJ_HD double sqrt_pos(double x) {
 #endif
 }
 
+// exp on the device: range reduction + degree-11 near-minimax polynomial +
+// ldexp (~1 ulp).  No special-case paths: ldexp overflows to inf above ~709
+// and underflows to 0 below ~-745, NaN stays NaN.  Used for the node loop's
+// exp(mu (1 - gamma)) and for n_e, T_e from their log splines.
+TORJ_HD double exp_fast(double x) {
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+    const double k = __builtin_rint(x * 1.4426950408889634074);
+    double r = fma(-k, 6.93147180559945286227e-01, x);
+    r = fma(-k, 2.31904681384629955842e-17, r);
+    // degree 11 near-minimax on |r| <= ln2/2 (tools/gen_exp_poly.py: 0.58 ulp,
+    // against 1.5 ulp for the degree 12 Taylor polynomial)
+    double p = 2.5100375832561234e-08;
+    p = fma(p, r, 2.7620075879983367e-07);
+    p = fma(p, r, 2.7557268480310024e-06);
+    p = fma(p, r, 2.4801521322368692e-05);
+    p = fma(p, r, 0.00019841269863040545);
+    p = fma(p, r, 0.0013888888917196719);
+    p = fma(p, r, 0.008333333333330065);
+    p = fma(p, r, 0.041666666666624164);
+    p = fma(p, r, 0.16666666666666669);
+    p = fma(p, r, 0.5000000000000001);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
+    // and ldexp of a huge negative exponent underflows to 0
+    int ki;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
+    return __builtin_amdgcn_ldexp(p, ki);
+#else
+    return exp(x);
+#endif
+}
+
 // Stencil position on one axis: clamped coordinate, cell index, weights.
 struct Axis {
     int i;
@@ -136,8 +169,11 @@ struct FieldPack {
 };
 
 // Evaluate fields [0, NGRAD) with gradients and [NGRAD, NGRAD+NVAL) value-only.
-// `fidx` maps pack slot -> coefficient field index.
-template <int NGRAD, int NVAL>
+// `fidx` maps pack slot -> coefficient field index.  EXT = false assumes the
+// point is inside the grid on both axes (Line() extrapolation distances 0) and
+// skips the sums only the extrapolation needs (value-only fields' slopes, the
+// mixed derivative); the results are then identical to EXT = true.
+template <int NGRAD, int NVAL, bool EXT = true>
 TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double R, double Z,
                          const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
     constexpr int NT = NGRAD + NVAL;
@@ -155,17 +191,20 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
         const double *row = coef + ((size_t)(aZ.i + b) * mR + aR.i) * kNF;
 #pragma unroll
         for (int f = 0; f < NT; f++) {
+            const bool slopes = EXT || f < NGRAD;
             double sv = 0.0, sd = 0.0;
 #pragma unroll
             for (int a = 0; a < 4; a++) {
                 const double c = row[a * kNF + fidx[f]];
                 sv = fma(aR.w[a], c, sv);
-                sd = fma(aR.dw[a], c, sd);
+                if (slopes) sd = fma(aR.dw[a], c, sd);
             }
             v[f] = fma(aZ.w[b], sv, v[f]);
-            gz[f] = fma(aZ.dw[b], sv, gz[f]);
-            gr[f] = fma(aZ.w[b], sd, gr[f]);
-            if (f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
+            if (slopes) {
+                gz[f] = fma(aZ.dw[b], sv, gz[f]);
+                gr[f] = fma(aZ.w[b], sd, gr[f]);
+            }
+            if (EXT && f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
         }
 #ifdef __HIP_DEVICE_COMPILE__
         // one stencil row in flight at a time: bounds the VGPRs held by
@@ -177,21 +216,44 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
 #pragma unroll
     for (int f = 0; f < NT; f++) {
         const double gR = gr[f] * g.invhR, gZ = gz[f] * g.invhZ;
-        out.v[f] = v[f] + aR.delta * gR + aZ.delta * gZ;
+        if constexpr (EXT) {
+            out.v[f] = v[f] + aR.delta * gR + aZ.delta * gZ;
+        } else {
+            out.v[f] = v[f];
+        }
         if (f < NGRAD) {
             const int q = f < NGRAD ? f : 0;
-            const double gRZ = grz[f] * (g.invhR * g.invhZ);
-            out.dR[q] = outR ? gR : gR + aZ.delta * gRZ;
-            out.dZ[q] = outZ ? gZ : gZ + aR.delta * gRZ;
+            if constexpr (EXT) {
+                const double gRZ = grz[f] * (g.invhR * g.invhZ);
+                out.dR[q] = outR ? gR : gR + aZ.delta * gRZ;
+                out.dZ[q] = outZ ? gZ : gZ + aR.delta * gRZ;
+            } else {
+                out.dR[q] = gR;
+                out.dZ[q] = gZ;
+            }
         }
     }
+}
+
+// Both coordinates inside the grid (no Line() extrapolation), for the whole
+// wave on the device: selects the EXT = false evaluation without divergence.
+TORJ_HD bool inside_grid(const Grid &g, double R, double Z) {
+    const bool in = R >= g.R1 && R <= g.Rn && Z >= g.Z1 && Z <= g.Zn;
+#ifdef __HIP_DEVICE_COMPILE__
+    return __all(in);
+#else
+    return in;
+#endif
 }
 
 // single value (e.g. psi for termination / deposition)
 TORJ_HD double eval_one(const double *__restrict__ coef, const Grid &g, double R, double Z, int field) {
     FieldPack<0, 1> p;
     const int idx[1] = {field};
-    eval_fields<0, 1>(coef, g, R, Z, idx, p);
+    if (inside_grid(g, R, Z))
+        eval_fields<0, 1, false>(coef, g, R, Z, idx, p);
+    else
+        eval_fields<0, 1, true>(coef, g, R, Z, idx, p);
     return p.v[0];
 }
 
@@ -280,13 +342,20 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     const double c = x[0] * invR, s = x[1] * invR;
     constexpr int NV = WITH_TE ? 1 : 0;
     FieldPack<4, NV> f;
+    const bool in = inside_grid(g, R, x[2]);
     if constexpr (WITH_TE) {
         const int idx[5] = {F_BR, F_BPHI, F_BZ, F_LNNE, F_LNTE};
-        eval_fields<4, 1>(coef, g, R, x[2], idx, f);
+        if (in)
+            eval_fields<4, 1, false>(coef, g, R, x[2], idx, f);
+        else
+            eval_fields<4, 1, true>(coef, g, R, x[2], idx, f);
         p.lnTe = f.v[4];
     } else {
         const int idx[4] = {F_BR, F_BPHI, F_BZ, F_LNNE};
-        eval_fields<4, 0>(coef, g, R, x[2], idx, f);
+        if (in)
+            eval_fields<4, 0, false>(coef, g, R, x[2], idx, f);
+        else
+            eval_fields<4, 0, true>(coef, g, R, x[2], idx, f);
         p.lnTe = 0.0;
     }
     const double Br = f.v[0], Bp = f.v[1], Bz = f.v[2];
@@ -312,7 +381,7 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     p.b[0] = Bx * invB;
     p.b[1] = By * invB;
     p.b[2] = Bz * invB;
-    const double ne = exp(f.v[3]);
+    const double ne = exp_fast(f.v[3]);
     p.ne = ne;
     p.X = ne * k.Cx;
     p.Y = Babs * k.Cy;
@@ -488,37 +557,6 @@ struct SeriesCoefs {
     }
 };
 
-// Node-loop elementary functions.  exp of a non-positive argument
-// (range reduction + degree-11 near-minimax, ~1 ulp; no overflow path; underflows to
-// 0 through ldexp).  Arguments here: 1 + u^2 >= 1 and mu (1 - gamma) <= 0.
-TORJ_HD double exp_nonpos(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
-    const double k = __builtin_rint(x * 1.4426950408889634074);
-    double r = fma(-k, 6.93147180559945286227e-01, x);
-    r = fma(-k, 2.31904681384629955842e-17, r);
-    // degree 11 near-minimax on |r| <= ln2/2 (tools/gen_exp_poly.py: 0.58 ulp,
-    // against 1.5 ulp for the degree 12 Taylor polynomial)
-    double p = 2.5100375832561234e-08;
-    p = fma(p, r, 2.7620075879983367e-07);
-    p = fma(p, r, 2.7557268480310024e-06);
-    p = fma(p, r, 2.4801521322368692e-05);
-    p = fma(p, r, 0.00019841269863040545);
-    p = fma(p, r, 0.0013888888917196719);
-    p = fma(p, r, 0.008333333333330065);
-    p = fma(p, r, 0.041666666666624164);
-    p = fma(p, r, 0.16666666666666669);
-    p = fma(p, r, 0.5000000000000001);
-    p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
-    // and ldexp of a huge negative exponent underflows to 0
-    int ki;
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
-    return __builtin_amdgcn_ldexp(p, ki);
-#else
-    return exp(x);
-#endif
-}
 
 #ifndef TORJ_PAIR_V2
 #define TORJ_PAIR_V2 1
@@ -550,11 +588,11 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double P = fma(A, fma(c.K3, t2, c.K0), fma(Cc, c.K1, -B));
     const double wp = w * p;
     const double a = fma(c.C1, t2, c.C0);
-    if (single) return wp * P * exp_nonpos(fma(-c.mu, sqrt_pos(a), c.mu));
+    if (single) return wp * P * exp_fast(fma(-c.mu, sqrt_pos(a), c.mu));
     const double Q = fma(A, c.K4, Cc * c.K5);
     const double b = c.C2 * t;
-    const double Ep = exp_nonpos(fma(-c.mu, sqrt_pos(a + b), c.mu));
-    const double Em = exp_nonpos(fma(-c.mu, sqrt_pos(a - b), c.mu));
+    const double Ep = exp_fast(fma(-c.mu, sqrt_pos(a + b), c.mu));
+    const double Em = exp_fast(fma(-c.mu, sqrt_pos(a - b), c.mu));
     return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 #else
@@ -580,12 +618,12 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double brp = A * fma(t, fma(c.K3, t, c.K4), c.K0) - B + Cc * fma(c.K5, t, c.K1);
     const double upp = fma(c.upa1, t, c.upa0);
     const double gp = sqrt_pos(fma(upp, upp, u_perp1));
-    double r = (wp * brp) * exp_nonpos(c.mu * (1.0 - gp));
+    double r = (wp * brp) * exp_fast(c.mu * (1.0 - gp));
     if (!single) {  // -t
         const double brm = A * fma(-t, fma(-c.K3, t, c.K4), c.K0) - B + Cc * fma(-c.K5, t, c.K1);
         const double upm = fma(-c.upa1, t, c.upa0);
         const double gm = sqrt_pos(fma(upm, upm, u_perp1));
-        r += (wp * brm) * exp_nonpos(c.mu * (1.0 - gm));
+        r += (wp * brm) * exp_fast(c.mu * (1.0 - gm));
     }
     return r;
 }
@@ -808,7 +846,7 @@ TORJ_HD void ray_rhs(const double *__restrict__ coef, const Grid &g, const Const
     dispersion_grad(p, N, mode, du, &Npar);
     if constexpr (ABS) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
+        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work);
     } else {
         alpha = 0.0;
     }

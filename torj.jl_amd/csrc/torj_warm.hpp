@@ -761,7 +761,7 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
     dispersion_grad(p, N, mode, du, &Npar, &inv);
     if constexpr (ABS == 1) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), mode, work);
+        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work);
     } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         alpha = alpha_warm_t<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode,
