@@ -32,6 +32,7 @@ sys.path.insert(0, os.path.join(ROOT, "torj.jl_amd"))
 
 # MI355X fp64 vector peak (spec): 256 CU x 2.4 GHz x 128 flop/clk (64 FMA lanes)
 FP64_VECTOR_PEAK_TFLOPS = 78.6
+HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 ABSORPTION = {"none": 0, "albajar": 1, "warm_wr": 2, "warm_fr": 3}
 ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)",
               "warm_wr": "warm weakly-relativistic alpha (iwarm=1)",
@@ -41,7 +42,7 @@ ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--n-rings", type=int, default=92)
     ap.add_argument("--min-az", type=int, default=11)
@@ -254,6 +255,9 @@ def main():
                 "frac": achieved / FP64_VECTOR_PEAK_TFLOPS if achieved is not None else None,
                 "traffic": traffic["traffic_bytes"] if traffic else None,
                 "traffic_source": traffic["file"] if traffic else None,
+                "hbm_GBps": traffic["traffic_bytes"] / kern_s / 1e9 if traffic else None,
+                "hbm_frac": traffic["traffic_bytes"] / kern_s / HBM_PEAK_BPS if traffic else None,
+                "valu_busy": traffic.get("valu_busy") if traffic else None,
                 "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
                 "deposition_kernels_ms": float(km[1].item()),
@@ -333,6 +337,13 @@ def measured_traffic(kname, n, args):
                 and wl.get("traj_stride") == args.traj_stride
                 and wl.get("absorption", "albajar") == args.absorption):
             t["file"] = os.path.relpath(f, ROOT)
+            # VALU-busy of the same profile: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
+            # (fraction of the hot kernel's wave-cycles issuing VALU)
+            try:
+                pmc = json.load(open(f.replace("traffic.json", "pmc_summary.json")))["avg"]
+                t["valu_busy"] = pmc["SQ_ACTIVE_INST_VALU"] / pmc["SQ_WAVE_CYCLES"]
+            except (OSError, ValueError, KeyError, ZeroDivisionError):
+                t["valu_busy"] = None
             return t
     return None
 
