@@ -690,6 +690,10 @@ __device__ __forceinline__ void sched_publish_begin() {
 
 // warm kernels: one wave per SIMD -- the 512-VGPR budget holds the warm
 // tensor without spills (C5: 458 vs 505 ms at two waves per SIMD)
+// rays per work-queue group (one wave's lanes; fewer leaves the upper lanes idle)
+#ifndef TORJ_GROUP
+#define TORJ_GROUP 64
+#endif
 #ifndef TORJ_WARM_MIN_WAVES
 #define TORJ_WARM_MIN_WAVES 1
 #endif
@@ -704,9 +708,9 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
         const unsigned t = sched_pop(ctl, slots, S, (unsigned)G);
         if (t == kGroupExit) break;
         const unsigned g = t & 0x7fffffffu;
-        const int i = (int)g * 64 + threadIdx.x;
+        const int i = (int)g * TORJ_GROUP + threadIdx.x;
         bool alive = false;
-        if (i < a.n) {
+        if (threadIdx.x < TORJ_GROUP && i < a.n) {
             RayState r;
             int ch = 0;
             if (t & 0x80000000u) {
@@ -1858,7 +1862,7 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         const char *e = getenv("TORJ_SCHED");
         return e ? atoi(e) : 1;
     }();
-    const int G = (n + 63) / 64;
+    const int G = (n + TORJ_GROUP - 1) / TORJ_GROUP;
     const int cs = cfg->chunk_steps > 0 ? cfg->chunk_steps : std::max(cfg->n_steps, 1);
     // default: the queue pays off once the beam exceeds one wave per SIMD
     // (measured: 42k rays 111 vs 106 ms one-shot; 100k rays 151 vs 174 ms)
