@@ -11,6 +11,7 @@
 // One lane evaluates one point; small tensors live in the lane's private
 // memory.  This is the heavy-VALU configuration C5 (~1e5 flop per alpha).
 #pragma once
+#include "torj_faddeeva_coefs.hpp"
 #include "torj_math.hpp"
 
 namespace torj {
@@ -356,7 +357,49 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
     }
     return {u, v};
 }
+// w(z) for Im z >= 0 by Weideman's rational approximation (N = 40,
+// tools/gen_faddeeva_coefs.py; 2.5e-14 relative to scipy's wofz): a fixed-cost
+// complex Horner sum with no branches, where TOMS 680 picks a series or a
+// continued fraction of data-dependent length per argument -- divergent across
+// a wave.  On the real axis Re w = exp(-x^2) exactly (as TOMS 680 sets it:
+// the absorption is that term).
+TORJ_HD cplx faddeeva_upper(double x, double y) {
+    constexpr double kInvSqrtPi = 0.56418958354775628695;
+    const double dr = kWeidL + y, di = -x;  // D = L - iz, Re D >= L > 0
+    const double id = rcp_nz(fma(dr, dr, di * di));
+    const double ir = dr * id, ii = -di * id;  // 1 / D
+    const double nr = kWeidL - y, ni = x;      // L + iz
+    const double Zr = fma(nr, ir, -ni * ii), Zi = fma(nr, ii, ni * ir);
+    double pr = kWeidA[0], pim = 0.0;
+#pragma unroll
+    for (int k = 1; k < kWeidN; k++) {
+        const double t = fma(pr, Zr, fma(-pim, Zi, kWeidA[k]));
+        pim = fma(pr, Zi, pim * Zr);
+        pr = t;
+    }
+    const double i2r = fma(ir, ir, -ii * ii), i2i = 2.0 * ir * ii;  // 1 / D^2
+    cplx w;
+    w.re = fma(2.0, fma(pr, i2r, -pim * i2i), kInvSqrtPi * ir);
+    w.im = fma(2.0, fma(pr, i2i, pim * i2r), kInvSqrtPi * ii);
+    if (y == 0.0) w.re = exp(-x * x);
+    return w;
+}
+
+#ifndef TORJ_FADDEEVA_WEIDEMAN
+#define TORJ_FADDEEVA_WEIDEMAN 1
+#endif
+// Z(z) = i sqrt(pi) w(z) (zetac, :345-465); the warm tensor's arguments all
+// have Im z >= 0 (zetac_upper); TOMS 680 serves Im z < 0
+TORJ_HD cplx zetac_upper(double x, double y) {
+#if TORJ_FADDEEVA_WEIDEMAN
+    const cplx w = faddeeva_upper(x, y);
+#else
+    const cplx w = faddeeva(x, y);
+#endif
+    return {-kSqrtPi * w.im, kSqrtPi * w.re};
+}
 TORJ_HD cplx zetac(double x, double y) {
+    if (y >= 0.0) return zetac_upper(x, y);
     const cplx w = faddeeva(x, y);
     return {-kSqrtPi * w.im, kSqrtPi * w.re};
 }
@@ -409,7 +452,7 @@ TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx
             if (kz == 1 && mirror) continue;
             const double zx = kz == 0 ? xp : (kz == 1 ? xm : x0);
             const double zy = kz == 0 ? yp : (kz == 1 ? ym : y0);
-            const cplx z = zetac(zx, zy);
+            const cplx z = zetac_upper(zx, zy);  // zy = 0 or phim >= 0
             if (kz == 0)
                 czp = z;
             else if (kz == 1)
