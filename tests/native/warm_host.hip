@@ -76,12 +76,6 @@ void fd_profile(int n, int n_steps, int n_psi, double ds, const double *grid, co
     fa.n_psi = n_psi;
     fa.ds = ds;
     fa.grid = grid;
-    const double dg = (grid[n_psi - 1] - grid[0]) / (n_psi - 1);
-    bool uni = dg > 0;
-    for (int k = 0; uni && k < n_psi; k++) uni = std::fabs(grid[k] - (grid[0] + k * dg)) <= 1e-9 * dg;
-    fa.uniform = uni;
-    fa.g0 = grid[0];
-    fa.ginv = uni ? 1.0 / dg : 0.0;
     fa.s0 = s0;
     fa.steps = steps;
     fa.smp_psi = smp_psi;

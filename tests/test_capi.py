@@ -121,3 +121,14 @@ def test_gpu_entry_points_fail_loudly_without_gpu(T, hplasma):
         T.trace(hplasma, [[2.2, 0, 0.2]], [[-0.9, 0, -0.4]], 6e11, 1, n_steps=10, absorption=False)
     with pytest.raises(T.TorjError):
         T.B_spline(hplasma, [2.0, 0.0, 0.1])
+
+
+def test_trace_rejects_non_increasing_psi_grid(T, hplasma):
+    """psi_dP_dV must be strictly increasing (the shell lookups assume it): the
+    host-pointer call checks its copy before any device work, so this runs on
+    CPU; the device-pointer call reports it through torj_trace_check (GPU test)."""
+    x = np.array([[2.3, 0.0, 0.1]])
+    N = np.array([[-0.9, 0.0, -0.3]])
+    grid = np.array([0.0, 0.5, 0.5, 1.0])
+    with pytest.raises(RuntimeError, match="strictly increasing"):
+        T.trace(hplasma, x, N, 2 * np.pi * 92.5e9, 1, n_steps=10, psi_grid=grid)

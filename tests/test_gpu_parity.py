@@ -382,3 +382,49 @@ def test_trace_on_129_grid(gpu, T, O):
     g = T.trace(hp, xp, Np, om, 1, ds=1e-4, n_steps=2000)
     o = op.trace(xp, Np, om, 1, 1e-4, 2000)
     _compare_trace(g, o)
+
+
+def test_device_pointer_trace_async_grid_check(gpu, T, hplasma, fan_states):
+    """torj_trace_device_ex on HBM tensors (the bench path, no host round trip):
+    bit-identical to the host-pointer call; a non-increasing psi grid is found on
+    the device and reported by torj_trace_check, not by a stream sync inside the
+    launch."""
+    import torch
+
+    xp, Np, w, om = fan_states[1]
+    xp, Np, w = xp[:96], Np[:96], w[:96]
+    n = len(w)
+    grid = np.linspace(0.0, 1.0, 200)
+    h = T.trace(hplasma, xp, Np, om, 1, n_steps=600, psi_grid=grid, weights=w)
+    dev = torch.device("cuda", 0)
+
+    def t(a, dtype=torch.float64):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dtype)
+
+    def run(g):
+        x0, N0, dw, dg = t(xp.T), t(Np.T), t(w), t(g)
+        state = torch.empty((7, n), dtype=torch.float64, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        steps = torch.empty(n, dtype=torch.int32, device=dev)
+        dP = torch.zeros(len(g) + 1, dtype=torch.float64, device=dev)
+        Pdep = torch.empty(n, dtype=torch.float64, device=dev)
+        cfg = T._lib.TraceCfg(om, 1, 1e-4, 600, 6, 1.0, 1e-6, 1, 0)
+        stream = torch.cuda.current_stream(dev)
+        L = T.lib()
+        T._lib.check(L.torj_trace_device_ex(hplasma.handle, cfg, n, x0.data_ptr(), N0.data_ptr(),
+                                            dw.data_ptr(), len(g), dg.data_ptr(), None, None,
+                                            state.data_ptr(), status.data_ptr(), steps.data_ptr(),
+                                            dP.data_ptr(), Pdep.data_ptr(), None, None,
+                                            stream.cuda_stream))
+        rc = L.torj_trace_check(hplasma.handle, stream.cuda_stream)
+        return rc, state.cpu().numpy().T, dP.cpu().numpy()
+
+    rc, state, dP = run(grid)
+    assert rc == 0
+    assert np.array_equal(state, h.state)
+    # binned shells are fp64 atomics: summation order differs between launches
+    assert np.abs(dP - h.dP_shell).max() <= 1e-12 * np.abs(h.dP_shell).max()
+    bad = grid.copy()
+    bad[50] = bad[49]
+    rc, _, _ = run(bad)
+    assert rc != 0 and b"strictly increasing" in T.lib().torj_last_error()

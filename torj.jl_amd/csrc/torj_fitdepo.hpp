@@ -37,8 +37,6 @@ struct FitArgs {
     int n, n_psi;  // rays, shell boundaries
     double ds;
     const double *grid;      // n_psi boundaries (ascending)
-    int uniform;             // grid[k] == g0 + k dg to rounding: direct index guess
-    double g0, ginv;
     const double *w;         // ray weights (n) or null
     const double *x_launch;  // 3 x n vacuum launch points (s = 0)
     const double *s0;        // n, vacuum path length to the entry point
@@ -149,25 +147,15 @@ TORJ_HD Cubic make_cubic(double y0, double y1, double M0, double M1, double h) {
     return q;
 }
 
-// smallest boundary index k with grid[k] > x (strict) / >= x
+// smallest boundary index k with grid[k] > x (strict) / >= x: a guess as if
+// the grid were uniform (np.linspace), corrected by a local walk -- exact for
+// any strictly increasing grid
 TORJ_HD int level_above(const FitArgs &a, double x, bool strict) {
-    int k;
-    if (a.uniform) {
-        const double u = (x - a.g0) * a.ginv;
-        k = u < 0 ? 0 : (u > a.n_psi ? a.n_psi : (int)ceil(u));
-        while (k > 0 && (strict ? a.grid[k - 1] > x : a.grid[k - 1] >= x)) k--;
-        while (k < a.n_psi && (strict ? a.grid[k] <= x : a.grid[k] < x)) k++;
-    } else {
-        int lo = 0, hi = a.n_psi;
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (strict ? a.grid[mid] > x : a.grid[mid] >= x)
-                hi = mid;
-            else
-                lo = mid + 1;
-        }
-        k = lo;
-    }
+    const double g0 = a.grid[0], gn = a.grid[a.n_psi - 1];
+    const double u = (x - g0) * ((double)(a.n_psi - 1) / (gn - g0));
+    int k = u < 0 ? 0 : (u > a.n_psi ? a.n_psi : (int)ceil(u));
+    while (k > 0 && (strict ? a.grid[k - 1] > x : a.grid[k - 1] >= x)) k--;
+    while (k < a.n_psi && (strict ? a.grid[k] <= x : a.grid[k] < x)) k++;
     return k;
 }
 

@@ -841,6 +841,13 @@ __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
     fit_depo_ray<kOpenCache>(a, i, psi_at(a.coef, a.g, xl));
 }
+// psi_dP_dV strictly increasing (the shell lookups assume it)
+__global__ void __launch_bounds__(256) k_grid_check(const double *grid, int n, int *flags) {
+    bool bad = false;
+    for (int k = threadIdx.x + 1; k < n; k += 256) bad |= !(grid[k] > grid[k - 1]);
+    if (bad) atomicOr(flags, 1);
+}
+
 __global__ void __launch_bounds__(256) k_shell_sum(FitArgs a) {
     const int k = blockIdx.x;
     double acc = 0.0;
@@ -1091,6 +1098,8 @@ struct torj_plasma_s {
     std::vector<hipEvent_t> ev_pool;       // 3 per recorded call (start, trace end, post end)
     size_t ev_used = 0;
     double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
+    int *d_flags = nullptr;        // launch error flags (bit 0: psi grid not strictly increasing)
+    bool last_depo = false;        // last torj_trace_device launch checked its psi grid
     size_t ws_cap = 0;
     int n_cu = 256;
     std::mutex mu;
@@ -1389,6 +1398,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
     if (p->d_fit) (void)hipFree(p->d_fit);
+    if (p->d_flags) (void)hipFree(p->d_flags);
     if (p->d_chunk) (void)hipFree(p->d_chunk);
     for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
@@ -1835,20 +1845,14 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         fa.s_uniform = cfg->integrator == 0;  // RK4: s_k = s0 + k ds, not stored
         fa.dP = dP;
         fa.Pray = Pdep;
-        // uniform boundaries (np.linspace) get a direct index guess, checked
-        // against the stored values; anything else is binary-searched
-        std::vector<double> hg(n_psi);
-        HIPCK(hipMemcpyAsync(hg.data(), grid, n_psi * sizeof(double), hipMemcpyDeviceToHost, s));
-        HIPCK(hipStreamSynchronize(s));
-        const double dg = (hg[n_psi - 1] - hg[0]) / (n_psi - 1);
-        bool uni = dg > 0;
-        for (int k = 0; uni && k < n_psi; k++)
-            uni = std::fabs(hg[k] - (hg[0] + k * dg)) <= 1e-9 * dg;
-        for (int k = 1; k < n_psi; k++)
-            if (!(hg[k] > hg[k - 1])) return fail("psi_dP_dV must be strictly increasing");
-        fa.uniform = uni;
-        fa.g0 = hg[0];
-        fa.ginv = uni ? 1.0 / dg : 0.0;
+        // boundary lookups guess from grid[0], grid[n-1] in-kernel and correct
+        // locally: no host read of the (device-resident) grid, no stream sync
+    }
+    p->last_depo = depo;
+    if (depo) {  // psi_dP_dV strictly increasing: checked on the device, reported by torj_trace_check
+        if (!p->d_flags) HIPCK(hipMalloc(&p->d_flags, sizeof(int)));
+        HIPCK(hipMemsetAsync(p->d_flags, 0, sizeof(int), s));
+        hipLaunchKernelGGL(k_grid_check, dim3(1), dim3(256), 0, s, grid, n_psi, p->d_flags);
     }
     const int DM = !depo ? kDepoNone : (fit ? kDepoSamples : kDepoBinned);
     if (tr) {
@@ -2030,9 +2034,12 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
                   int *steps, double *dP, double *Pdep, double *traj) {
     if (!p || !cfg) return fail("bad plasma handle or cfg");
     if (n <= 0) return 0;
+    const bool depo = n_psi >= 2 && grid;
+    if (depo)  // host copy at hand: checked before any device work
+        for (int k = 1; k < n_psi; k++)
+            if (!(grid[k] > grid[k - 1])) return fail("psi_dP_dV must be strictly increasing");
     if (ensure_device(p)) return -1;
     hipStream_t s = p->stream;
-    const bool depo = n_psi >= 2 && grid;
     const int n_save = cfg->traj_stride > 0 ? cfg->n_steps / cfg->traj_stride : 0;
     DevBufs B;
     double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dstate, *ddP = nullptr, *dPdep = nullptr,
@@ -2087,6 +2094,11 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
 int torj_trace_check(torj_plasma_t p, void *stream) {
     if (!p) return fail("bad plasma handle");
     HIPCK(hipStreamSynchronize((hipStream_t)stream));
+    if (p->last_depo && p->d_flags) {
+        int flags = 0;
+        HIPCK(hipMemcpy(&flags, p->d_flags, sizeof(int), hipMemcpyDeviceToHost));
+        if (flags & 1) return fail("psi_dP_dV must be strictly increasing");
+    }
     if (p->last_sched) {  // stall watchdog / retirement count of the work queue
         SchedCtl ctl;
         HIPCK(hipMemcpy(&ctl, p->d_sched, sizeof(ctl), hipMemcpyDeviceToHost));
