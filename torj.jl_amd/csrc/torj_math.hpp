@@ -206,11 +206,6 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
             }
             if (EXT && f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
         }
-#ifdef __HIP_DEVICE_COMPILE__
-        // one stencil row in flight at a time: bounds the VGPRs held by
-        // coefficient loads (the step is VALU-bound, not load-latency-bound)
-        __builtin_amdgcn_sched_barrier(0);
-#endif
     }
     const bool outR = aR.delta != 0.0, outZ = aZ.delta != 0.0;
 #pragma unroll
