@@ -66,6 +66,13 @@ def hplasma(T, eq):
 def gpu(T):
     import ctypes
 
+    # PyTorch-ROCm carries its own HIP runtime; when both share a process (the
+    # device-pointer tests, bench.py), torch's must initialise the device first
+    # -- after libtorj_hip's runtime has, torch reports no HIP GPU
+    import torch
+
+    if torch.cuda.is_available():
+        torch.cuda.init()
     n = ctypes.c_int(0)
     rc = T.lib().torj_device_count(ctypes.byref(n))
     if rc != 0 or n.value < 1:
