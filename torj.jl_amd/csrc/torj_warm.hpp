@@ -357,7 +357,7 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
     }
     return {u, v};
 }
-// w(z) for Im z >= 0 by Weideman's rational approximation (N = 40,
+// w(z) for Im z >= 0 by Weideman's rational approximation (N = 36,
 // tools/gen_faddeeva_coefs.py; 2.5e-14 relative to scipy's wofz): a fixed-cost
 // complex Horner sum with no branches, where TOMS 680 picks a series or a
 // continued fraction of data-dependent length per argument -- divergent across
