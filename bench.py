@@ -258,6 +258,12 @@ def main():
                 "hbm_GBps": traffic["traffic_bytes"] / kern_s / 1e9 if traffic else None,
                 "hbm_frac": traffic["traffic_bytes"] / kern_s / HBM_PEAK_BPS if traffic else None,
                 "valu_busy": traffic.get("valu_busy") if traffic else None,
+                # executed fp64 FLOPs of the same kernel and workload (PMC:
+                # SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes, FMA x 2)
+                "executed_TFLOPs": (traffic["fp64_flops_executed"] / kern_s / 1e12
+                                    if traffic and traffic.get("fp64_flops_executed") else None),
+                "frac_executed": (traffic["fp64_flops_executed"] / kern_s / 1e12 / FP64_VECTOR_PEAK_TFLOPS
+                                  if traffic and traffic.get("fp64_flops_executed") else None),
                 "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
                 "deposition_kernels_ms": float(km[1].item()),
