@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--absorption", choices=list(ABSORPTION), default="albajar",
                     help="albajar: abs_Albajar_fast (C3, the headline); warm_wr / warm_fr: the "
                          "repaired general_absorption.jl alpha, iwarm 1 (C5) / 3; none: cold")
+    ap.add_argument("--shard", action="store_true",
+                    help="C4 (strong scaling): split ONE fan across the ranks (contiguous ray "
+                         "ranges) instead of one rotated fan per rank; e.g. --n-rings 291 --shard "
+                         "for the ~1e6-ray beam over 8 GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
@@ -98,9 +102,14 @@ def main():
                                             setup["inverse_curvature_radius"], f,
                                             N_rings=args.n_rings,
                                             min_azimuthal_points=args.min_az)
-    phi = 2 * np.pi * rank / max(world, 1)  # weak scaling: each rank its own (rotated) beam
-    rot = np.array([[np.cos(phi), -np.sin(phi), 0], [np.sin(phi), np.cos(phi), 0], [0, 0, 1]])
-    pos, dirs = pos @ rot.T, dirs @ rot.T
+    n_fan = len(w)
+    if args.shard:  # strong scaling: this rank's contiguous slice of the one fan
+        lo, hi = rank * n_fan // world, (rank + 1) * n_fan // world
+        pos, dirs, w = pos[lo:hi], dirs[lo:hi], w[lo:hi]
+    else:  # weak scaling: each rank its own beam, rotated toroidally (axisymmetric plasma)
+        phi = 2 * np.pi * rank / max(world, 1)
+        rot = np.array([[np.cos(phi), -np.sin(phi), 0], [np.sin(phi), np.cos(phi), 0], [0, 0, 1]])
+        pos, dirs = pos @ rot.T, dirs @ rot.T
     t_entry = time.perf_counter()
     xp, Np, s0, st = T.ray_entry(plasma, pos, dirs, omega, args.mode, gpu=True)
     t_entry = time.perf_counter() - t_entry  # first call: includes device setup
@@ -228,17 +237,19 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.shard else "weak",
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic circular-tokamak equilibrium (analytic, sampled on 56x56) + "
                     "launch_peripheral_rays fan",
             "config": {
-                "workload": f"{'C5' if args.absorption.startswith('warm') else 'C3'}: {n}-ray EC fan per GPU (N_rings={args.n_rings}, "
+                "workload": f"{'C5' if args.absorption.startswith('warm') else ('C4' if args.shard else 'C3')}: "
+                            f"{(str(n_fan) + '-ray EC fan sharded over ' + str(world) + ' GPU(s)') if args.shard else (str(n) + '-ray EC fan per GPU')} (N_rings={args.n_rings}, "
                             f"min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, {args.n_steps} RK4 "
                             f"steps ds={args.ds:g} m ({args.integrator}), {ALPHA_NAME[args.absorption]}, psi-shell deposition "
                             f"n_psi={args.n_psi} ({args.deposition}), traj stride {args.traj_stride}",
                 "rays_per_gpu": n,
+                "rays_total": n_fan if args.shard else n * world,
                 "rk4_steps": args.n_steps,
                 "n_psi": args.n_psi,
                 "traj_stride": args.traj_stride,
