@@ -139,6 +139,9 @@ struct TraceArgs {
     double abstol, reltol, s_step;
     int n_chunks;
     int *chunk;  // n: chunks done (work-queue visits carry it)
+    // binned deposition in the work-queue kernel: per-wave LDS histogram of
+    // n_hist shells at dynamic-LDS offset hist_off (doubles); 0 = global atomics
+    int n_hist, hist_off;
 };
 
 // DEPO modes of the trace kernels
@@ -170,11 +173,23 @@ struct DepoAcc {
     double acc;
 };
 
+// a lane's finished run of deposits into one shell: the wave's LDS histogram
+// (flushed to dP once per queue visit) or, without one, a global atomic
+__device__ __forceinline__ void depo_flush(const TraceArgs &a, const DepoAcc &d) {
+    if (d.cur < 0) return;
+    if (a.n_hist > 0) {
+        extern __shared__ double lds_dyn[];
+        atomicAdd(lds_dyn + a.hist_off + d.cur, d.acc);
+    } else {
+        atomicAdd(a.dP + d.cur, d.acc);
+    }
+}
+
 __device__ __forceinline__ void depo_add(const TraceArgs &a, DepoAcc &d, int j, double v) {
     if (j == d.cur) {
         d.acc += v;
     } else {
-        if (d.cur >= 0) atomicAdd(a.dP + d.cur, d.acc);
+        depo_flush(a, d);
         d.cur = j;
         d.acc = v;
     }
@@ -333,7 +348,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
     }
     r.tau = tau;
     if constexpr (DEPO == kDepoBinned) {
-        if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
+        depo_flush(a, dacc);
     }
 }
 
@@ -590,7 +605,7 @@ __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r
         st = 1;
     }
     if constexpr (DEPO == kDepoBinned) {
-        if (dacc.cur >= 0) atomicAdd(a.dP + dacc.cur, dacc.acc);
+        depo_flush(a, dacc);
     }
 #pragma unroll
     for (int c = 0; c < 3; c++) {
@@ -704,6 +719,10 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
     extern __shared__ double lds_k[];  // integrator 1: Tsit5 stage vectors of this wave
     AlbajarWork work = {0u, 0u, 0u};
     unsigned long long steps = 0, nrhs = 0;
+    double *hist = lds_k + a.hist_off;  // binned deposition: this wave's shell histogram
+    if constexpr (DEPO == kDepoBinned) {
+        for (int k = threadIdx.x; k < a.n_hist; k += 64) hist[k] = 0.0;
+    }
     for (;;) {
         const unsigned t = sched_pop(ctl, slots, S, (unsigned)G);
         if (t == kGroupExit) break;
@@ -767,6 +786,19 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
             }
         }
         const bool any_alive = __any(alive);
+        if constexpr (DEPO == kDepoBinned) {  // the visit's shell sums: LDS -> dP
+            if (a.n_hist > 0) {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                for (int k = threadIdx.x; k < a.n_hist; k += 64) {
+                    const double v = hist[k];
+                    if (v != 0.0) {
+                        atomicAdd(a.dP + k, v);
+                        hist[k] = 0.0;
+                    }
+                }
+            }
+        }
         sched_publish_begin();
         if (threadIdx.x == 0) {
             if (any_alive) {
@@ -1949,13 +1981,18 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         p->last_groups = G;
         unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
         const dim3 grd(W), blk(64);
+        // binned shells: a per-wave LDS histogram (RK4, up to 4096 shells; the
+        // adaptive path's 25 KB of stage vectors leave no room without losing
+        // occupancy, it keeps the global atomics)
+        a.hist_off = adaptive ? kTsLds : 0;
+        a.n_hist = (DM == kDepoBinned && !adaptive && n_psi <= 4096) ? n_psi : 0;
+        const size_t lds = (size_t)(a.hist_off + a.n_hist) * sizeof(double);
 #define LAUNCH(A, D, T)                                                                            \
     do {                                                                                           \
         if (adaptive)                                                                              \
-            hipLaunchKernelGGL((k_trace_sched<A, D, T, 1>), grd, blk, kTsLds * sizeof(double), s, a, \
-                               ctl, slots, S, G, cs);                                              \
+            hipLaunchKernelGGL((k_trace_sched<A, D, T, 1>), grd, blk, lds, s, a, ctl, slots, S, G, cs); \
         else                                                                                       \
-            hipLaunchKernelGGL((k_trace_sched<A, D, T, 0>), grd, blk, 0, s, a, ctl, slots, S, G, cs); \
+            hipLaunchKernelGGL((k_trace_sched<A, D, T, 0>), grd, blk, lds, s, a, ctl, slots, S, G, cs); \
     } while (0)
         TORJ_DISPATCH_TRACE(LAUNCH);
 #undef LAUNCH
