@@ -230,9 +230,12 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
-/* Waits for `stream` and checks the last trace launched on this handle: for a
- * work-queue launch, that every ray group retired and the stall watchdog (no
- * progress anywhere in the grid for 120 s) did not fire.  torj_trace[_ex]
+/* Waits for `stream` and checks the last trace launched on this handle: that
+ * its psi_dP_dV grid was strictly increasing (checked on the device, so the
+ * _device calls never read device memory back or synchronise inside the
+ * launch; the host-pointer calls also check their host copy up front), and
+ * for a work-queue launch, that every ray group retired and the stall watchdog
+ * (no progress anywhere in the grid for 120 s) did not fire.  torj_trace[_ex]
  * call it themselves; callers of the asynchronous _device calls call it
  * before trusting the outputs. */
 int torj_trace_check(torj_plasma_t p, void *stream);
