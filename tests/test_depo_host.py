@@ -42,8 +42,8 @@ def _run(H, n_steps, grid, s0, steps, psiL, smp, nc, ds=1e-4):
     return dPs, kstar, P
 
 
-@pytest.mark.parametrize("mode", [1, -1])
-def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode):
+@pytest.mark.parametrize("mode,grid_kind", [(1, "uniform"), (-1, "uniform"), (1, "graded")])
+def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode, grid_kind):
     import deposition_ref as D
     from torj_hip import synthetic as S
 
@@ -55,7 +55,9 @@ def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode):
     om = 2 * np.pi * s["f_abs_test"]
     xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, mode)
     assert (st == 0).all()
-    grid = np.linspace(0, 1, 250)
+    # graded: boundaries packed towards the axis (the in-kernel lookup guesses as
+    # if uniform and walks to the right boundary)
+    grid = np.linspace(0, 1, 250) if grid_kind == "uniform" else np.linspace(0, 1, 250) ** 2
     n_steps = 3000
     o = oplasma.trace(xp, Np, om, mode, 1e-4, n_steps, psi_grid=grid, weights=w, samples=True, s0=s0)
     psiL = np.array([oplasma.evaluate("psi", p) for p in pos])
