@@ -226,8 +226,11 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * of it up to the summation order of dP_shell).  mode -1: default (env
  * TORJ_SCHED; else 1 when the beam has more
  * 64-ray groups than the device has SIMDs, otherwise 0); 0: one lane per ray for the whole trace; 1: persistent
- * waves pulling 64-ray groups chunk by chunk from a ready queue.  waves: number
- * of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
+ * waves pulling 64-ray groups chunk by chunk from a ready queue; 2: the whole
+ * trace with 16 lanes per ray (Albajar absorption, no binning: the node pairs
+ * of the absorption integral split between a ray's lanes, results equal to
+ * rounding; mode -1 picks it for beams of at most 2 x 64 x SIMDs / 16 rays).
+ * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
 /* Waits for `stream` and checks the last trace launched on this handle: that

@@ -428,3 +428,46 @@ def test_device_pointer_trace_async_grid_check(gpu, T, hplasma, fan_states):
     bad[50] = bad[49]
     rc, _, _ = run(bad)
     assert rc != 0 and b"strictly increasing" in T.lib().torj_last_error()
+
+
+@pytest.mark.parametrize("deposition", ["none", "reference"])
+def test_lanes_per_ray_bit_identical(gpu, T, hplasma, fan_states, deposition):
+    """Sixteen lanes per ray (small beams: the absorption's node pairs split
+    between a ray's lanes, summed back in the one-lane order) reproduces the
+    one-lane-per-ray kernel to rounding: a wave then holds 4 rays instead of 64,
+    and the Bessel polynomial length is chosen per wave (the longest any of its
+    rays needs), so alpha may come from a longer, equally accurate polynomial."""
+    xp, Np, w, om = fan_states[1]
+    idx = np.arange(0, len(w), 7)[:150]
+    grid = np.linspace(0, 1, 500)
+    kw = dict(ds=1e-4, n_steps=1500, traj_stride=100)
+    if deposition == "reference":
+        from torj_hip import synthetic as S
+
+        s = S.SETUP
+        N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+        pos, dirs, wf = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                                 s["inverse_curvature_radius"], s["f_abs_test"],
+                                                 N_rings=14, min_azimuthal_points=5)
+        xq, Nq, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1)
+        xp, Np, w = xq, Nq, wf
+        kw.update(psi_grid=grid, weights=w[idx], deposition="reference", x_launch=pos[idx],
+                  s0=s0[idx])
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp[idx], Np[idx], om, 1, **kw)
+        hplasma.set_sched(2)
+        b = T.trace(hplasma, xp[idx], Np[idx], om, 1, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    for f in ("status", "steps"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    sa, sb = np.asarray(a.state), np.asarray(b.state)
+    scale = np.abs(sa).max(axis=-1, keepdims=True) + 1e-300
+    assert (np.abs(sa - sb) / scale).max() <= 1e-12
+    for f in ("P_dep", "dP_shell"):
+        x, y = getattr(a, f), getattr(b, f)
+        assert np.abs(x - y).max() <= 1e-12 * max(np.abs(x).max(), 1e-300), f
+    fin = np.isfinite(a.traj)
+    assert np.array_equal(fin, np.isfinite(b.traj))
+    assert np.abs(a.traj[fin] - b.traj[fin]).max() <= 1e-12 * np.abs(a.traj[fin]).max()

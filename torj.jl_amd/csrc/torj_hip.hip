@@ -243,9 +243,14 @@ struct RayState {
 // src/solve.jl:154-177): classic RK4 of sys!, optical depth, chunk-boundary
 // termination, shell deposition, trajectory samples.  Shared by the one-shot
 // and the work-queue kernels.
-template <int ABS, int DEPO, bool TRAJ>
+// LPR > 1: the ray's LPR lanes integrate it together (identical state in every
+// lane; the absorption's node pairs are split between them) and lane sub = 0
+// does the ray's stores.
+template <int ABS, int DEPO, bool TRAJ, int LPR = 1>
 __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w, RayState &r,
-                                            int s_end, AlbajarWork &work) {
+                                            int s_end, AlbajarWork &work, int sub = 0) {
+    static_assert(LPR == 1 || (ABS == 1 && DEPO != kDepoBinned), "lanes per ray: Albajar, no binning");
+    const bool wr = LPR == 1 || sub == 0;
     const GLTable &gl = c_gl;
     double *x = r.x, *N = r.N;
     double tau = r.tau;
@@ -254,7 +259,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
     DepoAcc dacc = {-1, 0.0};
     if constexpr (DEPO != kDepoNone) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
     if constexpr (DEPO == kDepoSamples) {
-        if (r.steps == 0) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
+        if (r.steps == 0 && wr) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
             a.smp_psi[i] = psi_a;
             a.smp_dpds[i] = 0.0;  // arc lengths are implicit: s_k = s0 + k ds (FitArgs::S)
         }
@@ -271,7 +276,8 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         }
 #pragma unroll 1
         for (int st = 0; st < 4; st++) {
-            ray_rhs_m<ABS>(a.coef, a.g, a.k, gl, a.omega, a.mode, a.abs_model, xt, Nt, k, al, &work);
+            ray_rhs_m<ABS, LPR>(a.coef, a.g, a.k, gl, a.omega, a.mode, a.abs_model, xt, Nt, k, al,
+                                wr ? &work : nullptr, sub);
             const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
             const double h = (st < 2) ? hds : ds;
 #pragma unroll
@@ -303,7 +309,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if constexpr (DEPO == kDepoSamples) {
             // dP/ds at the saved point x_s = P_s alpha_approx(x_s) (src/solve.jl:171):
             // the stage-0 RHS of this step evaluated exactly that alpha (al0)
-            if (s > 0) a.smp_dpds[(size_t)s * a.n + i] = P * al0;
+            if (s > 0 && wr) a.smp_dpds[(size_t)s * a.n + i] = P * al0;
         }
 #pragma unroll
         for (int c = 0; c < 3; c++) {
@@ -318,14 +324,14 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if (DEPO != kDepoNone || check)
             psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
         if constexpr (DEPO == kDepoSamples) {
-            a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
+            if (wr) a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
         }
         if constexpr (DEPO == kDepoBinned) {
             r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
             psi_a = psi_b;
         }
         if constexpr (TRAJ) {
-            if (a.traj_stride > 0 && (r.steps % a.traj_stride) == 0) {
+            if (wr && a.traj_stride > 0 && (r.steps % a.traj_stride) == 0) {
                 const size_t si = (size_t)(r.steps / a.traj_stride - 1);
                 double *T = a.traj + si * 5 * (size_t)a.n + i;
                 T[0] = x[0];
@@ -393,20 +399,25 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
     }
 }
 
-// One-shot kernel: one lane per ray, all steps in one pass.
-template <int ABS, int DEPO, bool TRAJ>
+// One-shot kernel: LPR lanes per ray (1, or 16 for small beams whose rays
+// would leave most SIMDs idle: the node pairs of the absorption integral are
+// split between the ray's lanes), all steps in one pass.
+template <int ABS, int DEPO, bool TRAJ, int LPR = 1>
 __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int gt = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = gt / LPR, sub = gt % LPR;
     AlbajarWork work = {0u, 0u, 0u};
     unsigned long long steps = 0;
     if (i < a.n) {
         RayState r;
         load_start(a, i, r);
         const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
-        ray_segment<ABS, DEPO, TRAJ>(a, i, w, r, a.n_steps, work);
-        store_state(a, i, r);
-        if constexpr (DEPO == kDepoBinned) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
-        steps = r.steps;
+        ray_segment<ABS, DEPO, TRAJ, LPR>(a, i, w, r, a.n_steps, work, sub);
+        if (sub == 0) {
+            store_state(a, i, r);
+            if constexpr (DEPO == kDepoBinned) atomicAdd(a.dP + a.n_psi, w * r.Pdep);  // sum_rays w P_dep
+            steps = r.steps;
+        }
     }
     flush_counters(a, steps, 4ull * steps, work);
 }
@@ -1122,6 +1133,7 @@ struct torj_plasma_s {
     bool last_sched = false;               // last torj_trace_device launch used the work queue
     int last_groups = 0;                   // its number of 64-ray groups
     int sched_mode = -1, sched_waves = 0;  // torj_set_sched
+    int lanes_per_ray = 0;                 // one-shot kernel: 0 auto, 1 or 16 forced (torj_set_sched)
     int *d_chunk = nullptr;                // integrator 1: chunks done per ray
     size_t chunk_cap = 0;
     void *d_fit = nullptr;                 // reference-faithful deposition workspace
@@ -1998,10 +2010,31 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
 #undef LAUNCH
     } else {
         p->last_sched = false;
-        const dim3 grd(nblocks(n, TORJ_BLOCK)), blk(TORJ_BLOCK);
+        // small Albajar beams: 16 lanes per ray while n x 16 lanes fit two
+        // waves per SIMD (the latency of a ray's step chain sets the time there)
+        const bool split = cfg->absorption == 1 && DM != kDepoBinned && p->lanes_per_ray != 1 &&
+                           (p->lanes_per_ray == 16 ||
+                            (size_t)n * 16 <= (size_t)p->n_cu * 4 * 2 * 64);
+        const dim3 blk(TORJ_BLOCK);
+        if (split) {
+            const dim3 grd(nblocks(n * 16, TORJ_BLOCK));
+            if (DM == kDepoSamples) {
+                if (tr)
+                    hipLaunchKernelGGL((k_trace<1, kDepoSamples, true, 16>), grd, blk, 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_trace<1, kDepoSamples, false, 16>), grd, blk, 0, s, a);
+            } else {
+                if (tr)
+                    hipLaunchKernelGGL((k_trace<1, kDepoNone, true, 16>), grd, blk, 0, s, a);
+                else
+                    hipLaunchKernelGGL((k_trace<1, kDepoNone, false, 16>), grd, blk, 0, s, a);
+            }
+        } else {
+            const dim3 grd(nblocks(n, TORJ_BLOCK));
 #define LAUNCH(A, D, T) hipLaunchKernelGGL((k_trace<A, D, T>), grd, blk, 0, s, a)
-        TORJ_DISPATCH_TRACE01(LAUNCH);
+            TORJ_DISPATCH_TRACE01(LAUNCH);
 #undef LAUNCH
+        }
     }
     HIPCK(hipGetLastError());
     if (ev[1]) HIPCK(hipEventRecord(ev[1], s));
@@ -2051,9 +2084,10 @@ int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post
 
 int torj_set_sched(torj_plasma_t p, int mode, int waves) {
     if (!p) return fail("bad plasma handle");
-    if (mode < -1 || mode > 1) return fail("sched mode must be -1, 0 or 1");
+    if (mode < -1 || mode > 2) return fail("sched mode must be -1, 0, 1 or 2");
     if (waves < 0) return fail("waves must be >= 0");
-    p->sched_mode = mode;
+    p->sched_mode = mode == 2 ? 0 : mode;
+    p->lanes_per_ray = mode == 0 ? 1 : (mode == 2 ? 16 : 0);
     p->sched_waves = waves;
     return 0;
 }

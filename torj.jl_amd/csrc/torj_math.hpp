@@ -624,11 +624,42 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
 }
 #endif
 
-template <int M, int LV>
-TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c) {
+template <int M, int LV, int LPR = 1>
+TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     SeriesCoefs<M, LV> sc;
     sc.load();
     const int n = gl.n, half = n >> 1;
+#ifdef __HIP_DEVICE_COMPILE__
+    if constexpr (LPR > 1) {
+        // LPR lanes per ray (small beams, latency-bound): lane `sub` of the ray's
+        // group takes pairs sub, sub + LPR, ...; the group then adds the pair
+        // terms in the one-lane order 0, 1, 2, ... (each from its lane): every
+        // lane of the group holds the same sum, as LPR = 1 would compute it for
+        // the same polynomial length (chosen per wave, so it can differ)
+        constexpr int Q = (kMaxGL / 2 + LPR - 1) / LPR;
+        double rr[Q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            rr[q] = 0.0;
+            const int i = q * LPR + sub;
+            if (q * LPR < half && i < half)
+                rr[q] = pair_term<M, LV>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
+        }
+        const int base = (int)(threadIdx.x & 63u) & ~(LPR - 1);
+        double s = 0.0;
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            if (q * LPR >= half) break;
+#pragma unroll
+            for (int u = 0; u < LPR; u++) {
+                const double v = __shfl(rr[q], base + u, 64);
+                if (q * LPR + u < half) s += v;
+            }
+        }
+        if (n & 1) s += pair_term<M, LV>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
+        return s;
+    }
+#endif
     constexpr int U = TORJ_PAIR_UNROLL;
     double acc[U];
 #pragma unroll
@@ -691,10 +722,10 @@ struct AlbajarWork {
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
 // abs_Al_pol_fact) times sqrt((m/m_0)^2 - 1), WITHOUT the Maxwellian
 // normalisation a*(mu/2pi)^1.5 (common to both harmonics).
-template <int M>
+template <int M, int LPR = 1>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
                                 double inv_sqNp, double N_perp, double omega_bar,
-                                double Axz, double ea, double e3, AlbajarWork *work) {
+                                double Axz, double ea, double e3, AlbajarWork *work, int sub = 0) {
     constexpr double md = (double)M, inv_md = 1.0 / md;
     HarmConst c;
     c.r2m1 = r * r - 1.0;
@@ -729,11 +760,11 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     }
     double sum;
     switch (level) {
-        case 0: sum = node_sum<M, 0>(gl, c); break;
-        case 1: sum = node_sum<M, 1>(gl, c); break;
-        case 2: sum = node_sum<M, 2>(gl, c); break;
-        case 3: sum = node_sum<M, 3>(gl, c); break;
-        default: sum = node_sum<M, 4>(gl, c); break;
+        case 0: sum = node_sum<M, 0, LPR>(gl, c, sub); break;
+        case 1: sum = node_sum<M, 1, LPR>(gl, c, sub); break;
+        case 2: sum = node_sum<M, 2, LPR>(gl, c, sub); break;
+        case 3: sum = node_sum<M, 3, LPR>(gl, c, sub); break;
+        default: sum = node_sum<M, 4, LPR>(gl, c, sub); break;
     }
     // (m / (N_perp omega_bar))^2: IEEE quotient, N_perp = 0 (parallel
     // propagation) stays an infinity as in the reference
@@ -757,8 +788,9 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 #else
 #define TORJ_ALB_ATTR TORJ_HD
 #endif
+template <int LPR = 1>
 TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
-                                double N_par, double Te, int mode, AlbajarWork *work) {
+                                double N_par, double Te, int mode, AlbajarWork *work, int sub = 0) {
     if (Te < 20.0) return 0.0;
     constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te
     const double inv_mu = Te * (1.0 / kMuTe);
@@ -813,13 +845,13 @@ TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X,
     const double inv_m0 = inv_sqNp * Y;
     double c_abs = 0.0;
     if (!(2.0 < m_0)) {
-        c_abs += albajar_harmonic<2>(gl, mu, 2.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
-                                     Axz, ea, e3, work);
+        c_abs += albajar_harmonic<2, LPR>(gl, mu, 2.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
+                                          Axz, ea, e3, work, sub);
         if (work) work->n_harm++;
     }
     if (!(3.0 < m_0)) {  // src/absorption.jl:214 `if m < m_0 continue` (NaN m_0 -> NaN, as reference)
-        c_abs += albajar_harmonic<3>(gl, mu, 3.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
-                                     Axz, ea, e3, work);
+        c_abs += albajar_harmonic<3, LPR>(gl, mu, 3.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
+                                          Axz, ea, e3, work, sub);
         if (work) work->n_harm++;
     }
     // 1 / (1 + 105/(128 mu^2) + 15/(8 mu)), (mu / 2 pi)^1.5

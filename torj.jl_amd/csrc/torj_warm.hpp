@@ -794,17 +794,18 @@ TORJ_HD double alpha_warm(double omega, double X, double Y, double N_abs, double
 // one RHS evaluation: ABS 0 cold, 1 Albajar (abs_Albajar_fast), 2 warm weakly
 // relativistic (iwarm 1), 3 warm fully relativistic (iwarm 3); separate
 // instances keep each model's registers and private frame out of the others
-template <int ABS>
+template <int ABS, int LPR = 1>
 TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Consts &k,
                        const GLTable &gl, double omega, int mode, int model, const double x[3],
-                       const double N[3], double du[6], double &alpha, AlbajarWork *work) {
+                       const double N[3], double du[6], double &alpha, AlbajarWork *work,
+                       int sub = 0) {
     PlasmaPoint p;
     plasma_point<(ABS != 0)>(coef, g, k, x, p);
     double Npar, inv;
     dispersion_grad(p, N, mode, du, &Npar, &inv);
     if constexpr (ABS == 1) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work);
+        alpha = abs_albajar_fast<LPR>(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, sub);
     } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         alpha = alpha_warm_t<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode,

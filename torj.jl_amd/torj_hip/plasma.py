@@ -94,7 +94,8 @@ class Plasma:
         return out if np.ndim(psi) else float(out[0])
 
     def set_sched(self, mode: int = -1, waves: int = 0):
-        """torj_set_sched: -1 default, 0 one lane per ray, 1 ready-queue waves."""
+        """torj_set_sched: -1 default, 0 one lane per ray, 1 ready-queue waves,
+        2 sixteen lanes per ray (small beams; equal to rounding)."""
         check(lib().torj_set_sched(self._h, int(mode), int(waves)))
 
     def shell_volumes(self, psi_grid):
