@@ -217,7 +217,11 @@ def main():
         sched = adaptive or (os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd)
         dm = 2 if args.deposition == "reference" else 1
         at = min(ABSORPTION[args.absorption], 2)  # ABS template: 0 cold, 1 Albajar, 2 warm
+        # small Albajar beams run 16 lanes per ray (the library's automatic choice)
+        lpr16 = (not sched and at == 1 and dm == 2 and os.environ.get("TORJ_LPR", "0") != "1"
+                 and n * 16 <= n_simd * 2 * 64)
         kname = (f"k_trace_sched<{at}, {dm}, true, {int(adaptive)}>" if sched
+                 else f"k_trace<{at}, {dm}, true, 16>" if lpr16
                  else f"k_trace<{at}, {dm}, true>")  # rocprof's name of the instance
         traffic = measured_traffic(kname, n, args)
         kern_s = float(km[0].item()) / 1e3

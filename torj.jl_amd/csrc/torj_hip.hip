@@ -2012,9 +2012,14 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         p->last_sched = false;
         // small Albajar beams: 16 lanes per ray while n x 16 lanes fit two
         // waves per SIMD (the latency of a ray's step chain sets the time there)
+        // (TORJ_LPR=1 in the environment turns the automatic choice off)
+        static const int lpr_env = [] {
+            const char *e = getenv("TORJ_LPR");
+            return e ? atoi(e) : 0;
+        }();
         const bool split = cfg->absorption == 1 && DM != kDepoBinned && p->lanes_per_ray != 1 &&
                            (p->lanes_per_ray == 16 ||
-                            (size_t)n * 16 <= (size_t)p->n_cu * 4 * 2 * 64);
+                            (lpr_env != 1 && (size_t)n * 16 <= (size_t)p->n_cu * 4 * 2 * 64));
         const dim3 blk(TORJ_BLOCK);
         if (split) {
             const dim3 grd(nblocks(n * 16, TORJ_BLOCK));
