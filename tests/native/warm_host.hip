@@ -68,8 +68,15 @@ void wh_albajar(int n, const double *om, const double *X, const double *Y, const
 void fd_profile(int n, int n_steps, int n_psi, double ds, const double *grid, const double *s0,
                 const int *steps, const double *psiL, const double *smp_psi, const double *smp_dpds,
                 int nc, double *dPs, int *kstar, double *Pray) {
-    const size_t K = (size_t)n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
-    std::vector<double> E(K * N), G1(K * N), G2(K * N), Fo(L * N, NAN), dp(L * N, 0.0);
+    const size_t K = (size_t)n_steps + 2, N = (size_t)n, L = (size_t)n_psi, KN = torj::smp_elems(N, K);
+    std::vector<double> E(KN), G1(KN), G2(KN), Fo(L * N, NAN), dp(L * N, 0.0);
+    // the product's per-step layout (torj::smp_at: 64-ray blocks)
+    std::vector<double> sp(KN), sd(KN);
+    for (size_t j = 0; j <= (size_t)n_steps; j++)
+        for (size_t i = 0; i < N; i++) {
+            sp[torj::smp_at(j, (int)i, K)] = smp_psi[j * N + i];
+            sd[torj::smp_at(j, (int)i, K)] = smp_dpds[j * N + i];
+        }
     std::vector<int> cnt((L + 1) * N, 0);
     torj::FitArgs fa{};
     fa.n = n;
@@ -78,9 +85,10 @@ void fd_profile(int n, int n_steps, int n_psi, double ds, const double *grid, co
     fa.grid = grid;
     fa.s0 = s0;
     fa.steps = steps;
-    fa.smp_psi = smp_psi;
-    fa.smp_dpds = smp_dpds;
+    fa.smp_psi = sp.data();
+    fa.smp_dpds = sd.data();
     fa.smp_s = nullptr;
+    fa.rows = K;
     fa.s_uniform = 1;
     fa.E = E.data(), fa.Gpsi = G1.data(), fa.GP = G2.data();
     fa.cnt = cnt.data();

@@ -31,6 +31,18 @@
 
 namespace torj {
 
+// Per-step arrays of a ray (the trace kernel's samples, the elimination's
+// coefficients) in blocks of 64 rays: element (row j, ray i) at
+// ((i / 64) rows + j) 64 + i % 64.  A wave streams its block's rows as one
+// contiguous region instead of rows n x 8 B apart (a new page every few rows at
+// 1e5 rays: address-translation misses dominated the walk).  rows = n_steps + 2;
+// allocations hold ceil(n / 64) blocks.
+constexpr int kSmpBlk = 64;
+TORJ_HD size_t smp_at(size_t j, int i, size_t rows) {
+    return ((size_t)((unsigned)i / kSmpBlk) * rows + j) * kSmpBlk + (unsigned)i % kSmpBlk;
+}
+TORJ_HD size_t smp_elems(size_t n, size_t rows) { return (n + kSmpBlk - 1) / kSmpBlk * kSmpBlk * rows; }
+
 struct FitArgs {
     const double *coef;
     Grid g;
@@ -41,9 +53,10 @@ struct FitArgs {
     const double *x_launch;  // 3 x n vacuum launch points (s = 0)
     const double *s0;        // n, vacuum path length to the entry point
     const int *steps;        // n
-    const double *smp_psi, *smp_dpds, *smp_s;  // (n_steps + 1) x n (smp_s: arc length s_k)
+    const double *smp_psi, *smp_dpds, *smp_s;  // smp_at layout (smp_s: arc length s_k)
+    size_t rows;                       // smp_at rows per ray: n_steps + 2
     int s_uniform;                     // fixed-step RK4: s_k = s0 + k ds (smp_s unused)
-    double *E, *Gpsi, *GP;             // (n_steps + 2) x n backward-elimination coefficients
+    double *E, *Gpsi, *GP;             // smp_at layout: backward-elimination coefficients
     int *cnt;                          // (n_psi + 1) x n root-count differences per boundary
     double *Fopen;                     // (n_psi - 1) x n: F at a spilled open shell's root, NaN = closed
     double *dPs;                       // (n_psi - 1) x n: per-ray shell powers (before the break)
@@ -66,14 +79,14 @@ struct RayData {
     // fma the trajectory output uses), else the integrator's stored s
     TORJ_HD double S(int j) const {
         if (j == 0) return 0.0;
-        return a->s_uniform ? fma((double)(j - 1), a->ds, s0) : a->smp_s[(size_t)(j - 1) * a->n + i];
+        return a->s_uniform ? fma((double)(j - 1), a->ds, s0) : a->smp_s[smp_at(j - 1, i, a->rows)];
     }
     TORJ_HD double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
-    TORJ_HD double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[(size_t)(j - 1) * a->n + i]; }
-    TORJ_HD double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[(size_t)(j - 1) * a->n + i]; }
-    TORJ_HD double &EE(int j) const { return a->E[(size_t)j * a->n + i]; }
-    TORJ_HD double &GPSI(int j) const { return a->Gpsi[(size_t)j * a->n + i]; }
-    TORJ_HD double &GPP(int j) const { return a->GP[(size_t)j * a->n + i]; }
+    TORJ_HD double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[smp_at(j - 1, i, a->rows)]; }
+    TORJ_HD double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[smp_at(j - 1, i, a->rows)]; }
+    TORJ_HD double &EE(int j) const { return a->E[smp_at(j, i, a->rows)]; }
+    TORJ_HD double &GPSI(int j) const { return a->Gpsi[smp_at(j, i, a->rows)]; }
+    TORJ_HD double &GPP(int j) const { return a->GP[smp_at(j, i, a->rows)]; }
 };
 
 // not-a-knot cubic interpolation of psi and dP/ds (m >= 4 points): second
@@ -137,13 +150,13 @@ struct Cubic {  // y0 + t (b + t (c + t d)), t in [0, h]
     }
 };
 
-TORJ_HD Cubic make_cubic(double y0, double y1, double M0, double M1, double h) {
+TORJ_HD Cubic make_cubic(double y0, double y1, double M0, double M1, double h, double ih) {
     Cubic q;
     q.y0 = y0;
     q.h = h;
-    q.b = (y1 - y0) / h - h * (2.0 * M0 + M1) * (1.0 / 6.0);
+    q.b = (y1 - y0) * ih - h * (2.0 * M0 + M1) * (1.0 / 6.0);
     q.c = 0.5 * M0;
-    q.d = (M1 - M0) / (6.0 * h);
+    q.d = (M1 - M0) * ih * (1.0 / 6.0);
     return q;
 }
 
@@ -180,8 +193,10 @@ struct Cursor {
 
 // root of the monotone cubic piece q(t) = L on [ta, tb], L strictly between
 // the end values: Newton with a bisection safeguard, to the last bit
-TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, bool up) {
-    double lo = ta, hi = tb, t = 0.5 * (ta + tb);
+TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, double fa, double fb,
+                          bool up) {
+    double lo = ta, hi = tb, t = fma(L - fa, (tb - ta) * rcp_nz(fb - fa), ta);  // secant start
+    if (!(t > lo && t < hi)) t = 0.5 * (ta + tb);
     for (int it = 0; it < 100; it++) {
         const double v = q.f(t) - L;
         if (v == 0.0) break;
@@ -189,7 +204,7 @@ TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, bool u
             hi = t;  // past the root
         else
             lo = t;
-        double tn = t - v / q.df(t);
+        double tn = t - v * rcp_nz(q.df(t));
         if (!(tn > lo && tn < hi)) tn = 0.5 * (lo + hi);
         if (tn == t || !(tn > lo && tn < hi)) break;
         t = tn;
@@ -298,7 +313,13 @@ TORJ_HD void walk_segment(W_ &W, const Cubic &qs, double y1, const Cubic &qP, bo
     const double A = 3.0 * qs.d, B = 2.0 * qs.c, C = qs.b;
     const double disc = B * B - 4.0 * A * C;
     double c1 = qs.h, c2 = qs.h;
-    if (A != 0.0 ? disc > 0.0 : B != 0.0) {  // psi'(t) may vanish inside: split there
+    // psi'(0) = C and psi'(h) of one strict sign with the parabola's vertex
+    // -B / 2A outside (0, h): no zero inside, no split (the sqrt is skipped)
+    const double dh = fma(fma(A, qs.h, B), qs.h, C);
+    const double tv = -B * A;  // vertex position times 2 A^2
+    const bool keep = (C > 0.0 && dh > 0.0) || (C < 0.0 && dh < 0.0);
+    const bool vout = A == 0.0 || tv <= 0.0 || tv >= 2.0 * A * A * qs.h;
+    if (!(keep && vout) && (A != 0.0 ? disc > 0.0 : B != 0.0)) {  // psi'(t) may vanish inside: split there
         double r1 = NAN, r2 = NAN;
         if (A != 0.0) {
             const double sq = sqrt(disc);
@@ -346,7 +367,7 @@ TORJ_HD void walk_segment(W_ &W, const Cubic &qs, double y1, const Cubic &qP, bo
         }
         for (; d > 0 ? k < kend : k > kend; k += d) {
             const double L = a.grid[k];
-            const double t = (L == fb) ? tb : (L == fa ? ta : cubic_root(qs, L, ta, tb, d > 0));
+            const double t = (L == fb) ? tb : (L == fa ? ta : cubic_root(qs, L, ta, tb, fa, fb, d > 0));
             W.root(k, W.Fhi + (W.Flo + qP.G(t)), d);
         }
         fa = fb, ta = tb;
@@ -390,8 +411,8 @@ TORJ_HD void walk_ray(W_ &W, const RayData &R) {
         for (int u = 0; u < kWalkChunk; u++) {
             const int j = j0 + u;
             if (j + 1 >= m) break;
-            const double h = R.h(j);
-            const Cubic qs = make_cubic(yl, yv[u], Ml, Mr, h), qP = make_cubic(Pl, Pv[u], MPl, MPr, h);
+            const double h = R.h(j), ih = rcp_nz(h);
+            const Cubic qs = make_cubic(yl, yv[u], Ml, Mr, h, ih), qP = make_cubic(Pl, Pv[u], MPl, MPr, h, ih);
             walk_segment(W, qs, yv[u], qP, j == 0);
             yl = yv[u], Pl = Pv[u];
             // advance: (M_j, M_{j+1}, M_{j+2}) -> (M_{j+1}, M_{j+2}, M_{j+3})

@@ -130,9 +130,10 @@ struct TraceArgs {
     int n_save;
     double *traj;  // n_save x 4 x n
     unsigned long long *counters;
-    double *smp_psi;   // DEPO == 2: psi(x_k), (n_steps + 1) x n
-    double *smp_dpds;  // DEPO == 2: P_k alpha(x_k), (n_steps + 1) x n
-    double *smp_s;     // DEPO == 2: arc length s_k, (n_steps + 1) x n
+    double *smp_psi;   // DEPO == 2: psi(x_k), torj::smp_at layout
+    double *smp_dpds;  // DEPO == 2: P_k alpha(x_k), torj::smp_at layout
+    double *smp_s;     // DEPO == 2: arc length s_k, torj::smp_at layout
+    size_t smp_rows;   // rows per ray of the smp_at layout (n_steps + 2)
     int abs_model;     // 1 Albajar, 2 warm weakly relativistic, 3 warm fully relativistic
     const double *s0;  // n: arc length at the entry point (null: 0)
     // integrator 1 (the reference's adaptive solve)
@@ -260,8 +261,8 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
     if constexpr (DEPO != kDepoNone) psi_a = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
     if constexpr (DEPO == kDepoSamples) {
         if (r.steps == 0 && wr) {  // entry point: make_ray's dP_ds starts with 0 (src/solve.jl:151)
-            a.smp_psi[i] = psi_a;
-            a.smp_dpds[i] = 0.0;  // arc lengths are implicit: s_k = s0 + k ds (FitArgs::S)
+            a.smp_psi[smp_at(0, i, a.smp_rows)] = psi_a;
+            a.smp_dpds[smp_at(0, i, a.smp_rows)] = 0.0;  // arc lengths are implicit: s_k = s0 + k ds (FitArgs::S)
         }
     }
     const double ds = a.ds, hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
@@ -309,7 +310,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if constexpr (DEPO == kDepoSamples) {
             // dP/ds at the saved point x_s = P_s alpha_approx(x_s) (src/solve.jl:171):
             // the stage-0 RHS of this step evaluated exactly that alpha (al0)
-            if (s > 0 && wr) a.smp_dpds[(size_t)s * a.n + i] = P * al0;
+            if (s > 0 && wr) a.smp_dpds[smp_at(s, i, a.smp_rows)] = P * al0;
         }
 #pragma unroll
         for (int c = 0; c < 3; c++) {
@@ -324,7 +325,7 @@ __device__ __forceinline__ void ray_segment(const TraceArgs &a, int i, double w,
         if (DEPO != kDepoNone || check)
             psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
         if constexpr (DEPO == kDepoSamples) {
-            if (wr) a.smp_psi[(size_t)r.steps * a.n + i] = psi_b;
+            if (wr) a.smp_psi[smp_at(r.steps, i, a.smp_rows)] = psi_b;
         }
         if constexpr (DEPO == kDepoBinned) {
             r.Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
@@ -586,7 +587,7 @@ __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r
             if constexpr (DEPO != kDepoNone) {
                 const double psi_b = eval_one(a.coef, a.g, sqrt(u[0] * u[0] + u[1] * u[1]), u[2], F_PSI);
                 if constexpr (DEPO == kDepoSamples) {
-                    const size_t o = (size_t)r.steps * a.n + i;
+                    const size_t o = smp_at(r.steps, i, a.smp_rows);
                     a.smp_psi[o] = psi_b;
                     a.smp_dpds[o] = -K(0, 6);  // P alpha at the saved point (FSAL)
                     a.smp_s[o] = t;
@@ -777,9 +778,10 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
                     const int s0 = r.steps;
                     if constexpr (DEPO == kDepoSamples) {
                         if (ch == 0) {  // entry point (src/solve.jl:151)
-                            a.smp_psi[i] = eval_one(a.coef, a.g, sqrt(r.x[0] * r.x[0] + r.x[1] * r.x[1]), r.x[2], F_PSI);
-                            a.smp_dpds[i] = 0.0;
-                            a.smp_s[i] = a.s0 ? a.s0[i] : 0.0;
+                            const size_t o = smp_at(0, i, a.smp_rows);
+                            a.smp_psi[o] = eval_one(a.coef, a.g, sqrt(r.x[0] * r.x[0] + r.x[1] * r.x[1]), r.x[2], F_PSI);
+                            a.smp_dpds[o] = 0.0;
+                            a.smp_s[o] = a.s0 ? a.s0[i] : 0.0;
                         }
                     }
                     ch++;
@@ -872,13 +874,24 @@ __global__ void __launch_bounds__(64) k_final_alpha(TraceArgs a) {
         N[c] = a.state[(3 + c) * a.n + i];
     }
     if constexpr (ABS != 0) ray_rhs_m<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, a.abs_model, x, N, du, al, nullptr);
-    a.smp_dpds[(size_t)k * a.n + i] = exp(-a.state[6 * a.n + i]) * al;
+    a.smp_dpds[smp_at(k, i, a.smp_rows)] = exp(-a.state[6 * a.n + i]) * al;
 }
 
 // ---------------------------------------------------------------------------
 // Reference-faithful deposition (torj_fitdepo.hpp): one lane per ray
 // ---------------------------------------------------------------------------
+// boundaries up to this many are staged in LDS by k_fit_depo (32 KB per wave)
+constexpr int kFitGridLds = 4096;
+
 __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
+    // the walk's boundary lookups (cursor moves, root levels) form serial
+    // dependency chains: LDS latency instead of L2 latency on each
+    extern __shared__ double s_grid[];
+    if (a.n_psi <= kFitGridLds) {
+        for (int k = threadIdx.x; k < a.n_psi; k += 64) s_grid[k] = a.grid[k];
+        __syncthreads();
+        a.grid = s_grid;
+    }
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
@@ -1855,17 +1868,20 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         // samples (psi, dP/ds) per step, Thomas/second-derivative arrays,
         // per-boundary root counts, per-shell open-root integrals
         const size_t K = (size_t)cfg->n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
-        const size_t b_smp = 3 * K * N * sizeof(double), b_m = 3 * K * N * sizeof(double);
+        const size_t KN = smp_elems(N, K);  // smp_at layout: 64-ray blocks of K rows
+        const size_t b_smp = 3 * KN * sizeof(double), b_m = 3 * KN * sizeof(double);
         const size_t b_cnt = ((L + 1) * N * sizeof(int) + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
         const size_t b_ks = (N * sizeof(int) + 255) & ~(size_t)255;
         if (ensure_fit(p, b_smp + b_m + b_cnt + 2 * b_fo + b_ks)) return -1;
         char *base = (char *)p->d_fit;
         a.smp_psi = (double *)base;
-        a.smp_dpds = a.smp_psi + K * N;
-        a.smp_s = a.smp_dpds + K * N;
+        a.smp_dpds = a.smp_psi + KN;
+        a.smp_s = a.smp_dpds + KN;
+        a.smp_rows = K;
+        fa.rows = K;
         fa.E = (double *)(base + b_smp);
-        fa.Gpsi = fa.E + K * N;
-        fa.GP = fa.Gpsi + K * N;
+        fa.Gpsi = fa.E + KN;
+        fa.GP = fa.Gpsi + KN;
         fa.cnt = (int *)(base + b_smp + b_m);
         fa.Fopen = (double *)(base + b_smp + b_m + b_cnt);
         fa.dPs = fa.Fopen + L * N;
@@ -2054,7 +2070,8 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
             hipLaunchKernelGGL(k_final_alpha<1>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         else
             hipLaunchKernelGGL(k_final_alpha<0>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
-        hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), 0, s, fa);
+        const size_t lds = n_psi <= kFitGridLds ? (size_t)n_psi * sizeof(double) : 0;
+        hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), lds, s, fa);
         hipLaunchKernelGGL(k_shell_sum, dim3(n_psi), dim3(256), 0, s, fa);
         HIPCK(hipGetLastError());
     }
