@@ -9,6 +9,7 @@ timeout -k 10 900 python -m pytest tests -x -q -m gpu -p no:cacheprovider > $O/p
 tail -2 $O/pytest_gpu.log
 bash scripts/profile.sh prof_c3 || exit 1
 python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_trace || exit 1
+python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_fit_depo depo_ || exit 1
 bash scripts/profile.sh prof_c5 --absorption warm_wr || exit 1
 python tools/prof_summary.py gpurun_out/prof_c5 $O/profiles k_trace c5_ || exit 1
 cp $O/profiles/*.json $O/profiles/*.csv profiles/${ROUND:-r01}/ 2>/dev/null
