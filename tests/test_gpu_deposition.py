@@ -115,3 +115,23 @@ def test_make_ray_reference_deposition(gpu, T, hplasma, oplasma):
     assert np.abs(sv - svr).max() < 1e-12
     assert np.abs(dP_dV - prof).max() <= 1e-11 * np.abs(prof).max()
     assert abs(pdep - P) <= 1e-11 * P
+
+
+def test_reference_deposition_grid_beyond_lds(gpu, T, hplasma, oplasma):
+    """4 500 boundaries: more than k_fit_depo stages in LDS (kFitGridLds = 4096),
+    so the walk reads them from global memory; same FITPACK parity."""
+    import deposition_ref as D
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, 1, n_rings=2, min_az=3)
+    pos, xp, Np, s0, w = pos[:3], xp[:3], Np[:3], s0[:3], w[:3]
+    grid = np.linspace(0, 1, 4500)
+    kw = dict(ds=1e-4, n_steps=3000, psi_grid=grid, weights=w)
+    g = T.trace(hplasma, xp, Np, om, 1, deposition="reference", x_launch=pos, s0=s0, **kw)
+    o = oplasma.trace(xp, Np, om, 1, 1e-4, 3000, psi_grid=grid, weights=w, samples=True, s0=s0)
+    assert np.array_equal(g.steps, o["steps"])
+    shell, P = _ref_profile(D, oplasma, pos, s0, 1e-4, o, grid, w)
+    scale = np.abs(shell).max()
+    assert scale > 0
+    # a fine grid makes near-grazing boundaries likelier (see the test above)
+    assert np.abs(g.dP_shell[:-2] - shell).max() <= 1e-9 * scale
+    assert np.abs(g.P_dep - P).max() <= 1e-9 * max(P.max(), 1e-300)
