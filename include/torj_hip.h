@@ -229,7 +229,8 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * waves pulling 64-ray groups chunk by chunk from a ready queue; 2: the whole
  * trace with 16 lanes per ray (Albajar absorption, no binning: the node pairs
  * of the absorption integral split between a ray's lanes, results equal to
- * rounding; mode -1 picks it for beams of at most 2 x 64 x SIMDs / 16 rays).
+ * rounding; mode -1 picks it for beams of at most 2 x 64 x SIMDs / 16 rays
+ * unless env TORJ_LPR=1).
  * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
