@@ -117,6 +117,28 @@ def test_make_ray_reference_deposition(gpu, T, hplasma, oplasma):
     assert abs(pdep - P) <= 1e-11 * P
 
 
+@pytest.mark.parametrize("n_psi", [250, 4500])
+def test_reference_deposition_independent_of_scheduling(gpu, T, hplasma, n_psi):
+    """Reference deposition after the work-queue kernel (groups handed between
+    3 waves, samples written by different waves) is bit-identical to the one
+    after the one-lane kernel, with the boundaries staged in LDS (250) and read
+    from global memory (4 500)."""
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, 1, n_rings=8, min_az=7)
+    grid = np.linspace(0, 1, n_psi)
+    kw = dict(ds=1e-4, n_steps=3000, chunk_steps=150, psi_grid=grid, weights=w,
+              deposition="reference", x_launch=pos, s0=s0, traj_stride=100)
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        hplasma.set_sched(1, 3)  # 3 waves for the groups: hand-overs between waves
+        b = T.trace(hplasma, xp, Np, om, 1, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.abs(a.dP_shell).max() > 0
+
+
 def test_reference_deposition_grid_beyond_lds(gpu, T, hplasma, oplasma):
     """4 500 boundaries: more than k_fit_depo stages in LDS (kFitGridLds = 4096),
     so the walk reads them from global memory; same FITPACK parity."""
