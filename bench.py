@@ -297,7 +297,10 @@ def main():
             progress("host-pointer call done")
             out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(eq, xp, Np, w, omega, args, grid)
+            gpu_out = (d_state.cpu().numpy().T, status, d_steps.cpu().numpy())
+            out["cpu_baseline"], parity = cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out)
+            if parity is not None:
+                out["parity"] = parity
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -369,10 +372,13 @@ def measured_traffic(kname, n, args):
     return None
 
 
-def cpu_baseline(eq, xp, Np, w, omega, args, grid):
+def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
     """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same rays.
     Warm models: the C oracle's RK4 with oracle/warm_ref.py's numpy alpha through
-    a callback (serial), on a shorter sample (rays x steps sized to ~cpu_seconds)."""
+    a callback (serial), on a shorter sample (rays x steps sized to ~cpu_seconds).
+    Returns (cpu_baseline, parity): when the sample runs the full n_steps, parity
+    compares its endpoints with the timed launches' GPU outputs for the same rays
+    (status / steps exact, max relative error of x, N, tau; bar 1e-10)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from torj_hip import synthetic as S
@@ -404,13 +410,27 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid):
     r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, n_steps, weights=w[idx], **kw)
     dt = time.perf_counter() - t0
     steps = int(r["steps"].sum())
+    parity = None
+    if n_steps == args.n_steps and args.integrator == "rk4":
+        gs, gst, gk = (a[idx] for a in gpu_out)
+        os_ = r["state"]
+        ex = np.abs(gs[:, :3] - os_[:, :3]).max(1) / np.linalg.norm(os_[:, :3], axis=1)
+        eN = np.abs(gs[:, 3:6] - os_[:, 3:6]).max(1) / np.linalg.norm(os_[:, 3:6], axis=1)
+        et = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-300)
+        et[(gs[:, 6] == 0) & (os_[:, 6] == 0)] = 0.0
+        parity = {"rays": int(len(idx)), "vs": "oracle/torj_oracle.c (same RK4, same rays)",
+                  "status_equal": bool(np.array_equal(gst, r["status"])),
+                  "steps_equal": bool(np.array_equal(gk, r["steps"])),
+                  "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
+                  "max_rel_tau": float(et.max()),
+                  "max_rel": float(max(ex.max(), eN.max(), et.max())), "bar": 1e-10}
     what = ("oracle/torj_oracle.c RK4 + oracle/warm_ref.py numpy alpha (callback, serial)" if warm
             else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_rays} rays (evenly spaced over the same fan) x {n_steps} RK4 steps, "
                       f"{what}, {steps} ray-steps in {dt:.1f} s (ray stepping "
                       f"+ binned deposition; the reference profile's FITPACK post-processing is "
-                      f"not included on the CPU side)"}
+                      f"not included on the CPU side)"}, parity
 
 
 if __name__ == "__main__":

@@ -1,0 +1,176 @@
+// Warm-absorption check harness (test infrastructure, not the product).
+//
+//   warm_check host        host build only: alpha_warm / dieltens_* over a seeded
+//                          point set, for running under -fsanitize=address,undefined
+//                          (tests/native/Makefile target warm_check_asan)
+//   warm_check gpu         the same points on the device through three entry
+//                          shapes -- alpha_warm inlined into the kernel (what the
+//                          trace kernels do), alpha_warm behind a noinline call
+//                          (DESIGN.md 3.6's formerly wrong variant) and the fully
+//                          relativistic tensor behind a noinline call -- each
+//                          compared with the host build; prints the worst
+//                          relative difference per variant and exits 1 above 1e-9.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "torj_warm.hpp"
+
+using namespace torj;
+
+struct Pt {
+    double om, X, Y, Nabs, Npar, Te, inv;
+    int mode, iwarm;
+};
+
+__device__ __attribute__((noinline)) double alpha_warm_noinline(double om, double X, double Y,
+                                                               double Na, double Np, double Te,
+                                                               double inv, int mode, int iwarm,
+                                                               cplx *n2) {
+    return alpha_warm(om, X, Y, Na, Np, Te, inv, mode, iwarm, n2);
+}
+
+__device__ __attribute__((noinline)) void dieltens_fr_noinline(double X, double Y, double Np,
+                                                               double mu, int lrm,
+                                                               Tensor<kWarmMaxL> *T) {
+    dieltens_fr<kWarmMaxL>(X, Y, Np, mu, lrm, *T);
+}
+
+__global__ void k_alpha(const Pt *p, int n, int variant, double *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Pt q = p[i];
+    cplx n2 = C(0.0);
+    double a;
+    if (variant == 0)
+        a = alpha_warm(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm, &n2);
+    else
+        a = alpha_warm_noinline(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm, &n2);
+    out[3 * i] = a, out[3 * i + 1] = n2.re, out[3 * i + 2] = n2.im;
+}
+
+__global__ void k_tensor_fr(const Pt *p, int n, Tensor<kWarmMaxL> *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Pt q = p[i];
+    const double mu = kMe * kC * kC / (q.Te * kE);
+    const int lrm = std::min(larmornumber(q.Y, q.Npar, mu), kWarmMaxL);
+    Tensor<kWarmMaxL> T;
+    for (int l = 0; l < kWarmMaxL; l++)
+        for (int c = 0; c < 6; c++) T.e[l][c] = C(0.0);
+    dieltens_fr_noinline(q.X, q.Y, q.Npar, mu, lrm, &T);
+    out[i] = T;
+}
+
+static std::vector<Pt> points(int n) {
+    std::mt19937_64 rng(12345);
+    std::uniform_real_distribution<double> u(0.0, 1.0);
+    std::vector<Pt> v;
+    // the input of DESIGN.md 3.6 (formerly wrong behind a noinline call)
+    v.push_back({879645943005.1421, 0.6356810078139615, 1.123386636357144, 1.1218582593493804,
+                 -0.04727651004849054, 6785.414288396569, 1.1316334434814521, 1, 3});
+    for (int i = 0; i < n; i++) {
+        Pt q;
+        q.om = 2 * kPi * 140e9;
+        q.X = 0.05 + 0.85 * u(rng);
+        q.Y = 0.3 + 1.1 * u(rng);
+        q.Npar = -0.5 + u(rng);
+        q.Te = pow(10.0, 1.0 + 3.3 * u(rng));
+        q.inv = 0.2 + 1.8 * u(rng);
+        q.mode = (i & 1) ? 1 : -1;
+        q.iwarm = (i & 2) ? 3 : 1;
+        q.Nabs = sqrt(q.Npar * q.Npar + 0.2 + 0.9 * u(rng));
+        v.push_back(q);
+    }
+    return v;
+}
+
+static double host_alpha(const Pt &q, cplx &n2) {
+    return alpha_warm(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm, &n2);
+}
+
+static double rel(double a, double b, double scale) {
+    if (a == b) return 0.0;
+    if (std::isnan(a) && std::isnan(b)) return 0.0;
+    return fabs(a - b) / (fabs(b) + scale);
+}
+
+int main(int argc, char **argv) {
+    const bool gpu = argc > 1 && !strcmp(argv[1], "gpu");
+    const int n = argc > 2 ? atoi(argv[2]) : 2000;
+    std::vector<Pt> P = points(n);
+    const int m = (int)P.size();
+    std::vector<double> ha(m), hr(m), hi(m);
+    std::vector<Tensor<kWarmMaxL>> hT(m);
+    for (int i = 0; i < m; i++) {
+        cplx c;
+        ha[i] = host_alpha(P[i], c);
+        hr[i] = c.re, hi[i] = c.im;
+        const double mu = kMe * kC * kC / (P[i].Te * kE);
+        const int lrm = std::min(larmornumber(P[i].Y, P[i].Npar, mu), kWarmMaxL);
+        for (int l = 0; l < kWarmMaxL; l++)
+            for (int c2 = 0; c2 < 6; c2++) hT[i].e[l][c2] = C(0.0);
+        dieltens_fr<kWarmMaxL>(P[i].X, P[i].Y, P[i].Npar, mu, lrm, hT[i]);
+    }
+    double s = 0;
+    for (int i = 0; i < m; i++) s += ha[i] + hr[i] + hi[i];
+    printf("host: %d points, checksum %.17g, point 0 alpha %.15e n2 (%.15e, %.15e)\n", m, s, ha[0],
+           hr[0], hi[0]);
+    if (!gpu) return 0;
+
+    Pt *dP;
+    double *dout;
+    Tensor<kWarmMaxL> *dT;
+    if (hipMalloc(&dP, m * sizeof(Pt)) || hipMalloc(&dout, 3 * m * sizeof(double)) ||
+        hipMalloc(&dT, m * sizeof(Tensor<kWarmMaxL>)))
+        return 2;
+    if (hipMemcpy(dP, P.data(), m * sizeof(Pt), hipMemcpyHostToDevice)) return 2;
+    int bad = 0;
+    std::vector<double> o(3 * m);
+    for (int variant = 0; variant < 2; variant++) {
+        hipLaunchKernelGGL(k_alpha, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, variant, dout);
+        if (hipDeviceSynchronize() || hipMemcpy(o.data(), dout, 3 * m * sizeof(double), hipMemcpyDeviceToHost))
+            return 3;
+        double ea = 0, en = 0;
+        int wa = 0;
+        for (int i = 0; i < m; i++) {
+            // alpha floor: 1e-9 of its N_perp^2 scale (as tests/test_gpu_warm.py)
+            const double fl = 1e-9 * 2.0 * std::hypot(hr[i], hi[i]) * P[i].om / kC * P[i].inv;
+            const double e1 = rel(o[3 * i], ha[i], fl + 1e-300);
+            const double e2 = std::max(rel(o[3 * i + 1], hr[i], 1e-300), rel(o[3 * i + 2], hi[i], 1e-12 * fabs(hr[i]) + 1e-300));
+            if (e1 > ea) ea = e1, wa = i;
+            en = std::max(en, e2);
+        }
+        printf("%s: max rel alpha %.3e (point %d: dev %.15e host %.15e), max rel N_perp^2 %.3e\n",
+               variant ? "alpha_warm noinline" : "alpha_warm inlined", ea, wa, o[3 * wa], ha[wa], en);
+        if (ea > 1e-9 || en > 1e-9) bad = 1;
+    }
+    std::vector<Tensor<kWarmMaxL>> gT(m);
+    hipLaunchKernelGGL(k_tensor_fr, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, dT);
+    if (hipDeviceSynchronize() || hipMemcpy(gT.data(), dT, m * sizeof(Tensor<kWarmMaxL>), hipMemcpyDeviceToHost))
+        return 3;
+    double et = 0;
+    int wt = 0, wl = 0, wc = 0;
+    for (int i = 0; i < m; i++) {
+        double sc = 0;
+        for (int l = 0; l < kWarmMaxL; l++)
+            for (int c = 0; c < 6; c++) sc = std::max(sc, std::max(fabs(hT[i].e[l][c].re), fabs(hT[i].e[l][c].im)));
+        for (int l = 0; l < kWarmMaxL; l++)
+            for (int c = 0; c < 6; c++) {
+                const double e = std::max(fabs(gT[i].e[l][c].re - hT[i].e[l][c].re),
+                                          fabs(gT[i].e[l][c].im - hT[i].e[l][c].im)) / (sc + 1e-300);
+                if (e > et) et = e, wt = i, wl = l, wc = c;
+            }
+    }
+    printf("dieltens_fr noinline: max diff / tensor scale %.3e (point %d, l %d, c %d: dev (%.6e, %.6e) host (%.6e, %.6e))\n",
+           et, wt, wl + 1, wc, gT[wt].e[wl][wc].re, gT[wt].e[wl][wc].im, hT[wt].e[wl][wc].re, hT[wt].e[wl][wc].im);
+    if (et > 1e-9) bad = 1;
+    printf(bad ? "FAIL\n" : "OK\n");
+    return bad;
+}

@@ -1,0 +1,88 @@
+"""GPU parity at the headline workload itself (BASELINE configs[2], SURVEY.md
+§8(d) C3): the full 100 203-ray 92/11 fan, X-mode 92.5 GHz, 2 000 RK4 steps of
+1e-4 m, Albajar alpha, the reference deposition on a 1 000-point psi grid --
+traced with the library's DEFAULT scheduling, i.e. the work-queue kernel
+k_trace_sched with its production wave count (~1 566 groups over ~1 468
+persistent waves), the regime bench.py times.
+
+Checks (tolerances as tests/test_gpu_parity.py):
+  * every 25th ray (4 009 rays) against the CPU oracle: status and step counts
+    exact, x, N, tau <= 1e-10 relative;
+  * per-ray deposited power of 24 evenly spaced rays against the FITPACK
+    restatement of power_deposition_profile (oracle/deposition_ref.py) <= 1e-11;
+  * the whole beam against the one-lane-per-ray kernel (set_sched(0)): every
+    per-ray output bit-identical, dP_shell to the order of its fp64 sums;
+  * sum_j w P_dep = dP_shell[n_psi] (make_beam's deposited power).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+N_RINGS, MIN_AZ, N_STEPS, DS = 92, 11, 2000, 1e-4
+
+
+@pytest.fixture(scope="module")
+def c3(gpu, T, hplasma):
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    f = s["f_abs_test"]
+    om = 2 * np.pi * f
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=N_RINGS,
+                                            min_azimuthal_points=MIN_AZ)
+    assert len(w) == 100203
+    xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1, gpu=True)
+    assert (st == T.OK).all()
+    grid = np.linspace(0.0, 1.0, 1000)
+    kw = dict(ds=DS, n_steps=N_STEPS, psi_grid=grid, weights=w, traj_stride=100,
+              deposition="reference", x_launch=pos, s0=s0)
+    hplasma.set_sched(-1)  # the default: work queue with the production wave count
+    g = T.trace(hplasma, xp, Np, om, 1, **kw)
+    return dict(pos=pos, xp=xp, Np=Np, s0=s0, w=w, om=om, grid=grid, kw=kw, g=g)
+
+
+def test_c3_fan_sampled_parity(c3, oplasma):
+    """Every 25th ray of the headline beam vs the oracle (1e-10, exact statuses)."""
+    from test_gpu_parity import _compare_trace
+
+    g, idx = c3["g"], np.arange(0, len(c3["w"]), 25)
+    o = oplasma.trace(c3["xp"][idx], c3["Np"][idx], c3["om"], 1, DS, N_STEPS,
+                      psi_grid=c3["grid"], weights=c3["w"][idx])
+    sub = type(g)(g.state[idx], g.status[idx], g.steps[idx], None, None, None)
+    _compare_trace(sub, o)
+    # most of the beam is absorbed within the 0.2 m path (X2 layer)
+    assert np.median(g.P_end) < 0.1
+    assert abs(g.dP_shell[-1] - np.dot(c3["w"], g.P_dep)) <= 1e-12 * g.dP_shell[-1]
+
+
+def test_c3_fan_reference_deposition_vs_fitpack(c3, oplasma):
+    """P_dep of 24 rays of the work-queue run vs FITPACK's power_deposition_profile."""
+    import deposition_ref as D
+
+    g = c3["g"]
+    idx = np.linspace(0, len(c3["w"]) - 1, 24).astype(int)
+    o = oplasma.trace(c3["xp"][idx], c3["Np"][idx], c3["om"], 1, DS, N_STEPS, samples=True,
+                      s0=c3["s0"][idx])
+    assert np.array_equal(o["steps"], g.steps[idx])
+    for k, i in enumerate(idx):
+        sv, psi, dpds = D.ray_vectors(c3["pos"][i], c3["s0"][i], DS, o["steps"][k],
+                                      o["samples"][k], oplasma.evaluate("psi", c3["pos"][i]))
+        _, P = D.power_deposition_profile(sv, psi, dpds, c3["grid"], oplasma.volume)
+        assert abs(g.P_dep[i] - P) <= 1e-11 * max(P, 1e-300), (i, g.P_dep[i], P)
+
+
+def test_c3_fan_work_queue_equals_one_lane(c3, T, hplasma):
+    """Production work queue vs the one-lane-per-ray kernel on the whole beam."""
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, c3["xp"], c3["Np"], c3["om"], 1, **c3["kw"])
+    finally:
+        hplasma.set_sched(-1)
+    b = c3["g"]
+    for f in ("state", "status", "steps", "P_dep"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
