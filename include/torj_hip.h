@@ -221,6 +221,26 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
                          double *state, int *status, int *steps, double *dP_shell, double *P_dep,
                          double *traj, uint64_t *counters, void *stream);
 
+/* make_beam's fan-out and reduce across the GPUs of this process
+ * (src/solve.jl:209-240: one task per ray, then sum_i w_i dP_dV_i and
+ * sum_i w_i P_i).  Host pointers, the arguments and outputs of torj_trace_ex.
+ * The rays are cut into n_shards contiguous shards (0: one per GPU; at least
+ * n_gpus), their boundaries on 64-ray multiples, dealt round-robin to n_gpus
+ * devices: device (p's device + k) mod the device count for k < n_gpus, each
+ * with its own copy of the plasma, stream and host thread.  A device runs its
+ * shards in turn (upload, trace, deposition, download, torj_trace_check), its
+ * dP_shell partial accumulating on the device; the partials are summed over
+ * the devices by one RCCL all-reduce of n_psi + 1 fp64 (single-process
+ * communicator from ncclCommInitAll, kept on the handle; n_gpus = 1 needs no
+ * reduce unless env TORJ_BEAM_RCCL=1).  Per-ray outputs equal torj_trace_ex's
+ * for the same rays and scheduling; dP_shell differs by summation order only.
+ * Errors name the failing device. */
+int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                    const double *N0, const double *weights, int n_psi, const double *psi_grid,
+                    const double *x_launch, const double *s0, double *state, int *status,
+                    int *steps, double *dP_shell, double *P_dep, double *traj, int n_gpus,
+                    int n_shards);
+
 /* Scheduling of torj_trace / torj_trace_device launches on this plasma handle
  * (no reference counterpart: an MI355X tuning knob; results are independent
  * of it up to the summation order of dP_shell).  mode -1: default (env
@@ -234,14 +254,17 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
-/* Waits for `stream` and checks the last trace launched on this handle: that
- * its psi_dP_dV grid was strictly increasing (checked on the device, so the
- * _device calls never read device memory back or synchronise inside the
- * launch; the host-pointer calls also check their host copy up front), and
- * for a work-queue launch, that every ray group retired and the stall watchdog
- * (no progress anywhere in the grid for 120 s) did not fire.  torj_trace[_ex]
- * call it themselves; callers of the asynchronous _device calls call it
- * before trusting the outputs. */
+/* Waits for `stream` and checks every trace launched on this handle since
+ * the previous check (the flags are sticky: each launch ORs its outcome in,
+ * this call reads and clears them): that each psi_dP_dV grid was strictly
+ * increasing (checked on the device, so the _device calls never read device
+ * memory back or synchronise inside the launch; the host-pointer calls also
+ * check their host copy up front), and for work-queue launches, that every ray
+ * group retired and the stall watchdog (no progress anywhere in the grid for
+ * 120 s) did not fire.  torj_trace[_ex] call it themselves; callers of the
+ * asynchronous _device calls call it before trusting the outputs.  All
+ * _device calls on one handle must use one stream: they share the handle's
+ * scratch (work queue, deposition workspace). */
 int torj_trace_check(torj_plasma_t p, void *stream);
 
 /* Per-phase HIP-event timing of torj_trace[_device][_ex] calls on this handle

@@ -15,6 +15,7 @@
 // prefilter), the launch fan and the ray entry -- setup work the reference also
 // does per beam/ray on the CPU.
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -23,6 +24,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/torj_hip.h"
@@ -897,6 +899,14 @@ __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
     fit_depo_ray<kOpenCache>(a, i, psi_at(a.coef, a.g, xl));
 }
+// a work-queue launch's outcome into the handle's sticky flags (bit 1 stall
+// watchdog, bit 2 not every group retired); read by torj_trace_check
+__global__ void k_sched_fold(const SchedCtl *ctl, unsigned G, int *flags) {
+    int f = 0;
+    if (ctl->err) f |= 2;
+    if (ctl->finished != G) f |= 4;
+    if (f) atomicOr(flags, f);
+}
 // psi_dP_dV strictly increasing (the shell lookups assume it)
 __global__ void __launch_bounds__(256) k_grid_check(const double *grid, int n, int *flags) {
     bool bad = false;
@@ -1143,8 +1153,6 @@ struct torj_plasma_s {
     hipStream_t stream = nullptr;
     void *d_sched = nullptr;  // work-queue control block + ready-queue ring (zeroed per launch)
     size_t sched_cap = 0;
-    bool last_sched = false;               // last torj_trace_device launch used the work queue
-    int last_groups = 0;                   // its number of 64-ray groups
     int sched_mode = -1, sched_waves = 0;  // torj_set_sched
     int lanes_per_ray = 0;                 // one-shot kernel: 0 auto, 1 or 16 forced (torj_set_sched)
     int *d_chunk = nullptr;                // integrator 1: chunks done per ray
@@ -1155,11 +1163,18 @@ struct torj_plasma_s {
     std::vector<hipEvent_t> ev_pool;       // 3 per recorded call (start, trace end, post end)
     size_t ev_used = 0;
     double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
-    int *d_flags = nullptr;        // launch error flags (bit 0: psi grid not strictly increasing)
-    bool last_depo = false;        // last torj_trace_device launch checked its psi grid
+    // sticky launch error flags, ORed by every launch since the last
+    // torj_trace_check (which reads and clears them): bit 0 psi grid not
+    // strictly increasing, bit 1 work-queue watchdog, bit 2 unretired groups
+    int *d_flags = nullptr;
     size_t ws_cap = 0;
     int n_cu = 256;
     std::mutex mu;
+    // torj_trace_beam: handles of the same plasma on further devices (replica k
+    // on device (device + k) mod count; k = 0 is this handle) and the
+    // single-process RCCL communicator over the first nccl_n of them
+    std::vector<torj_plasma_s *> replicas;
+    std::vector<ncclComm_t> comms;
 };
 
 static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
@@ -1202,6 +1217,8 @@ static int ensure_device(torj_plasma_s *p) {
                     hipMemcpyHostToDevice));
     HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     HIPCK(hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, p->device));
+    HIPCK(hipMalloc(&p->d_flags, sizeof(int)));
+    HIPCK(hipMemset(p->d_flags, 0, sizeof(int)));
     return 0;
 }
 
@@ -1450,6 +1467,8 @@ int torj_plasma_create_from_coefs(int nR, int nZ, double R1, double Rn, double Z
 
 int torj_plasma_destroy(torj_plasma_t p) {
     if (!p) return 0;
+    for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
+    for (size_t k = 1; k < p->replicas.size(); k++) torj_plasma_destroy(p->replicas[k]);
     if (p->d_coef) (void)hipSetDevice(p->device);
     if (p->d_coef) (void)hipFree(p->d_coef);
     if (p->stream) (void)hipStreamDestroy(p->stream);
@@ -1908,12 +1927,8 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         // boundary lookups guess from grid[0], grid[n-1] in-kernel and correct
         // locally: no host read of the (device-resident) grid, no stream sync
     }
-    p->last_depo = depo;
-    if (depo) {  // psi_dP_dV strictly increasing: checked on the device, reported by torj_trace_check
-        if (!p->d_flags) HIPCK(hipMalloc(&p->d_flags, sizeof(int)));
-        HIPCK(hipMemsetAsync(p->d_flags, 0, sizeof(int), s));
+    if (depo)  // psi_dP_dV strictly increasing: checked on the device, reported by torj_trace_check
         hipLaunchKernelGGL(k_grid_check, dim3(1), dim3(256), 0, s, grid, n_psi, p->d_flags);
-    }
     const int DM = !depo ? kDepoNone : (fit ? kDepoSamples : kDepoBinned);
     if (tr) {
         a.traj_stride = cfg->traj_stride;
@@ -2005,8 +2020,6 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         if (ensure_sched(p, bytes)) return -1;
         HIPCK(hipMemsetAsync(p->d_sched, 0, bytes, s));
         SchedCtl *ctl = (SchedCtl *)p->d_sched;
-        p->last_sched = true;
-        p->last_groups = G;
         unsigned long long *slots = (unsigned long long *)((char *)p->d_sched + 256);
         const dim3 grd(W), blk(64);
         // binned shells: a per-wave LDS histogram (RK4, up to 4096 shells; the
@@ -2024,8 +2037,9 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     } while (0)
         TORJ_DISPATCH_TRACE(LAUNCH);
 #undef LAUNCH
+        // the queue's watchdog / retirement state into the sticky flags
+        hipLaunchKernelGGL(k_sched_fold, dim3(1), dim3(1), 0, s, ctl, (unsigned)G, p->d_flags);
     } else {
-        p->last_sched = false;
         // small Albajar beams: 16 lanes per ray while n x 16 lanes fit two
         // waves per SIMD (the latency of a ray's step chain sets the time there)
         // (TORJ_LPR=1 in the environment turns the automatic choice off)
@@ -2184,21 +2198,224 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
     return torj_trace_check(p, s);
 }
 
+// ---- make_beam across the GPUs of this process (src/solve.jl:209-240) -----
+// Replica k of a plasma handle: the same coefficients on device (device + k)
+// mod the device count, with its own stream, scratch and scheduling copy.
+static int beam_replicas(torj_plasma_s *p, int n_gpus) {
+    int ndev = 0;
+    HIPCK(hipGetDeviceCount(&ndev));
+    if (n_gpus < 1 || n_gpus > ndev)
+        return fail("n_gpus = %d, but %d HIP devices are visible", n_gpus, ndev);
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->replicas.empty()) p->replicas.push_back(p);
+    while ((int)p->replicas.size() < n_gpus) {
+        auto *q = new torj_plasma_s();
+        q->device = (p->device + (int)p->replicas.size()) % ndev;
+        q->g = p->g;
+        q->coef = p->coef;
+        q->n_vol = p->n_vol;
+        q->v1 = p->v1;
+        q->vn = p->vn;
+        q->vol_coef = p->vol_coef;
+        q->psi_prof_max = p->psi_prof_max;
+        p->replicas.push_back(q);
+    }
+    for (int k = 1; k < n_gpus; k++) {  // scheduling knobs follow the base handle
+        p->replicas[k]->sched_mode = p->sched_mode;
+        p->replicas[k]->sched_waves = p->sched_waves;
+        p->replicas[k]->lanes_per_ray = p->lanes_per_ray;
+    }
+    return 0;
+}
+
+// Contiguous shard k of S over n rays, boundaries on 64-ray (one wave, one
+// work-queue group) multiples, so every shard holds the same 64-ray groups as
+// the unsplit beam and per-ray results do not depend on the split.
+static void beam_shard(int n, int S, int k, int &lo, int &cnt) {
+    const long G = (n + 63) / 64;
+    const long g0 = G * k / S, g1 = G * (k + 1) / S;
+    lo = (int)std::min<long>(g0 * 64, n);
+    cnt = (int)std::min<long>(g1 * 64, n) - lo;
+}
+
+// One device's share: its shards in sequence on the replica's stream, with
+// dP_shell accumulated on the device (d_dP, zeroed here) for the reduce.
+static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S, int k0, int dk,
+                       const double *x0, const double *N0, const double *w, int n_psi,
+                       const double *grid, const double *xl, const double *s0, double *state,
+                       int *status, int *steps, double *P_dep, double *traj, double *d_dP) {
+    if (ensure_device(q)) return -1;
+    hipStream_t s = q->stream;
+    const bool depo = n_psi >= 2 && grid;
+    const int n_save = cfg->traj_stride > 0 ? cfg->n_steps / cfg->traj_stride : 0;
+    int m = 0;  // largest shard of this device
+    for (int k = k0; k < S; k += dk) {
+        int lo, cnt;
+        beam_shard(n, S, k, lo, cnt);
+        m = std::max(m, cnt);
+    }
+    if (depo) HIPCK(hipMemsetAsync(d_dP, 0, (n_psi + 1) * sizeof(double), s));
+    if (m == 0) return 0;
+    DevBufs B;
+    double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dxl = nullptr, *ds0 = nullptr, *dstate,
+                       *dPdep = nullptr, *dtraj = nullptr;
+    int *dstatus, *dsteps;
+    if (dalloc(&dx0, 3 * (size_t)m, true) || dalloc(&dN0, 3 * (size_t)m, true) ||
+        dalloc(&dstate, 7 * (size_t)m, true) || dalloc(&dstatus, m, true) || dalloc(&dsteps, m, true) ||
+        dalloc(&dw, m, w != nullptr) || dalloc(&dxl, 3 * (size_t)m, xl != nullptr) ||
+        dalloc(&ds0, m, s0 != nullptr) || dalloc(&dPdep, m, depo) ||
+        dalloc(&dtraj, (size_t)n_save * 5 * m, traj && n_save > 0))
+        return -1;
+    B.track(dx0), B.track(dN0), B.track(dstate), B.track(dstatus), B.track(dsteps), B.track(dw);
+    B.track(dxl), B.track(ds0), B.track(dPdep), B.track(dtraj);
+    if (depo) {
+        if (dupload(&dgrid, grid, n_psi, s)) return -1;
+        B.track(dgrid);
+    }
+    const size_t D = sizeof(double);
+    // rows x cnt sub-block of a (rows x n) SoA host array <-> compact (rows x cnt) device array
+    auto up = [&](double *d, const double *h, int rows, int lo, int cnt) -> int {
+        if (!d || !h) return 0;
+        HIPCK(hipMemcpy2DAsync(d, cnt * D, h + lo, (size_t)n * D, cnt * D, rows, hipMemcpyHostToDevice, s));
+        return 0;
+    };
+    auto down = [&](double *h, const double *d, int rows, int lo, int cnt) -> int {
+        if (!d || !h) return 0;
+        HIPCK(hipMemcpy2DAsync(h + lo, (size_t)n * D, d, cnt * D, cnt * D, rows, hipMemcpyDeviceToHost, s));
+        return 0;
+    };
+    for (int k = k0; k < S; k += dk) {
+        int lo, cnt;
+        beam_shard(n, S, k, lo, cnt);
+        if (cnt == 0) continue;
+        if (up(dx0, x0, 3, lo, cnt) || up(dN0, N0, 3, lo, cnt) || up(dw, w, 1, lo, cnt) ||
+            up(dxl, xl, 3, lo, cnt) || up(ds0, s0, 1, lo, cnt))
+            return -1;
+        if (torj_trace_device_ex(q, cfg, cnt, dx0, dN0, w ? dw : nullptr, depo ? n_psi : 0, dgrid,
+                                 xl ? dxl : nullptr, s0 ? ds0 : nullptr, dstate, dstatus, dsteps,
+                                 depo ? d_dP : nullptr, dPdep, traj && n_save > 0 ? dtraj : nullptr,
+                                 nullptr, s))
+            return -1;
+        if (down(state, dstate, 7, lo, cnt) || down(P_dep, depo ? dPdep : nullptr, 1, lo, cnt) ||
+            down(traj, traj && n_save > 0 ? dtraj : nullptr, n_save * 5, lo, cnt) ||
+            ddownload(status + lo, dstatus, cnt, s) || ddownload(steps + lo, dsteps, cnt, s))
+            return -1;
+        // this shard's queue / grid flags, before the replica's scratch is reused
+        if (torj_trace_check(q, s)) return -1;
+    }
+    return 0;
+}
+
+int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                    const double *N0, const double *weights, int n_psi, const double *grid,
+                    const double *x_launch, const double *s0, double *state, int *status,
+                    int *steps, double *dP, double *Pdep, double *traj, int n_gpus, int n_shards) {
+    if (!p || !cfg) return fail("bad plasma handle or cfg");
+    if (n < 0 || n_shards < 0) return fail("n and n_shards must be >= 0");
+    if (n == 0) {
+        if (dP && n_psi > 0) std::fill(dP, dP + n_psi + 1, 0.0);
+        return 0;
+    }
+    if (!x0 || !N0 || !state || !status || !steps) return fail("x0, N0, state, status, steps required");
+    const bool depo = n_psi >= 2 && grid;
+    if (depo) {
+        for (int k = 1; k < n_psi; k++)
+            if (!(grid[k] > grid[k - 1])) return fail("psi_dP_dV must be strictly increasing");
+        if (!dP || !Pdep) return fail("deposition needs dP_shell and P_dep");
+    }
+    if (beam_replicas(p, n_gpus)) return -1;
+    const int S = std::max(n_shards > 0 ? n_shards : n_gpus, n_gpus);
+    const char *rccl_e = getenv("TORJ_BEAM_RCCL");  // read per call (tests toggle it)
+    const bool rccl_env = rccl_e && atoi(rccl_e) != 0;
+    const bool rccl = depo && (n_gpus > 1 || rccl_env);
+    // per-device partial dP_shell, reduced by one RCCL all-reduce
+    std::vector<double *> d_dP(n_gpus, nullptr);
+    std::vector<std::string> errs(n_gpus);
+    std::vector<int> rc(n_gpus, 0);
+    auto run = [&](int k) {
+        torj_plasma_s *q = p->replicas[k];
+        rc[k] = -1;
+        if (hipSetDevice(q->device) != hipSuccess) {
+            errs[k] = "hipSetDevice failed";
+            return;
+        }
+        if (depo && hipMalloc(&d_dP[k], (n_psi + 1) * sizeof(double)) != hipSuccess) {
+            errs[k] = "hipMalloc of the dP_shell partial failed";
+            return;
+        }
+        rc[k] = beam_worker(q, cfg, n, S, k, n_gpus, x0, N0, weights, n_psi, grid, x_launch, s0,
+                            state, status, steps, depo ? Pdep : nullptr, traj, d_dP[k]);
+        if (rc[k]) errs[k] = g_err;
+    };
+    if (n_gpus == 1) {
+        run(0);
+    } else {  // one host thread per device: each drives its own stream
+        std::vector<std::thread> th;
+        for (int k = 0; k < n_gpus; k++) th.emplace_back(run, k);
+        for (auto &t : th) t.join();
+    }
+    int out = 0;
+    for (int k = 0; k < n_gpus && !out; k++)
+        if (rc[k]) out = fail("torj_trace_beam, device %d: %s", p->replicas[k]->device, errs[k].c_str());
+    if (!out && depo) {
+        if (rccl) {
+            // make_beam's reduce (src/solve.jl:233-240): sum of the (n_psi+1)
+            // partials over the devices, RCCL over xGMI, single-process communicator
+            if ((int)p->comms.size() != n_gpus) {
+                for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
+                p->comms.assign(n_gpus, nullptr);
+                std::vector<int> devs(n_gpus);
+                for (int k = 0; k < n_gpus; k++) devs[k] = p->replicas[k]->device;
+                if (ncclCommInitAll(p->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
+                    p->comms.clear();
+                    out = fail("ncclCommInitAll over %d devices failed", n_gpus);
+                }
+            }
+            if (!out) {
+                ncclResult_t r = ncclGroupStart();
+                for (int k = 0; k < n_gpus && r == ncclSuccess; k++)
+                    r = ncclAllReduce(d_dP[k], d_dP[k], (size_t)n_psi + 1, ncclDouble, ncclSum,
+                                      p->comms[k], p->replicas[k]->stream);
+                const ncclResult_t r2 = ncclGroupEnd();
+                if (r != ncclSuccess || r2 != ncclSuccess)
+                    out = fail("ncclAllReduce of dP_shell failed: %s",
+                               ncclGetErrorString(r != ncclSuccess ? r : r2));
+            }
+        }
+        if (!out) {
+            torj_plasma_s *q0 = p->replicas[0];
+            if (hipSetDevice(q0->device) != hipSuccess ||
+                hipMemcpyAsync(dP, d_dP[0], (n_psi + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                               q0->stream) != hipSuccess ||
+                hipStreamSynchronize(q0->stream) != hipSuccess)
+                out = fail("download of dP_shell failed");
+        }
+    }
+    for (int k = 0; k < n_gpus; k++)
+        if (d_dP[k]) {
+            (void)hipSetDevice(p->replicas[k]->device);
+            (void)hipStreamSynchronize(p->replicas[k]->stream);
+            (void)hipFree(d_dP[k]);
+        }
+    if (!out && !depo) {
+        if (dP) std::fill(dP, dP + (n_psi > 0 ? n_psi + 1 : 1), 0.0);
+        if (Pdep) std::fill(Pdep, Pdep + n, 0.0);
+    }
+    (void)hipSetDevice(p->device);
+    return out;
+}
+
 int torj_trace_check(torj_plasma_t p, void *stream) {
     if (!p) return fail("bad plasma handle");
+    if (!p->d_flags) return 0;  // no launch yet
+    HIPCK(hipSetDevice(p->device));
     HIPCK(hipStreamSynchronize((hipStream_t)stream));
-    if (p->last_depo && p->d_flags) {
-        int flags = 0;
-        HIPCK(hipMemcpy(&flags, p->d_flags, sizeof(int), hipMemcpyDeviceToHost));
-        if (flags & 1) return fail("psi_dP_dV must be strictly increasing");
-    }
-    if (p->last_sched) {  // stall watchdog / retirement count of the work queue
-        SchedCtl ctl;
-        HIPCK(hipMemcpy(&ctl, p->d_sched, sizeof(ctl), hipMemcpyDeviceToHost));
-        if (ctl.err) return fail("work-queue watchdog fired (ready-queue stalled)");
-        if (ctl.finished != (unsigned)p->last_groups)
-            return fail("work queue retired %u of %d ray groups", ctl.finished, p->last_groups);
-    }
+    int flags = 0;  // ORed by every launch on this handle since the last check
+    HIPCK(hipMemcpy(&flags, p->d_flags, sizeof(int), hipMemcpyDeviceToHost));
+    if (flags) HIPCK(hipMemset(p->d_flags, 0, sizeof(int)));
+    if (flags & 1) return fail("psi_dP_dV must be strictly increasing");
+    if (flags & 2) return fail("work-queue watchdog fired (ready-queue stalled)");
+    if (flags & 4) return fail("work queue did not retire every ray group");
     return 0;
 }
 

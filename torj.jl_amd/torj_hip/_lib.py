@@ -76,6 +76,8 @@ _SIGS = {
                              _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_trace_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                                 _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
+    "torj_trace_beam": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
+                                  _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp, C.c_int, C.c_int]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "torj_trace_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),

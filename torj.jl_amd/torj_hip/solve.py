@@ -77,7 +77,7 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
           absorption=True, psi_grid=None, weights=None, traj_stride: int = 0,
           deposition: str = "binned", x_launch=None, s0=None, integrator: str = "rk4",
           abstol: float = 1e-6, reltol: float = 1e-6, s_max: float | None = None,
-          n_chunks: int = 100) -> TraceResult:
+          n_chunks: int = 100, n_gpus: int | None = None, n_shards: int = 0) -> TraceResult:
     """Integrate rays from in-plasma start states (x0, N0: (n, 3)) on the GPU.
 
     deposition="binned": psi-shell binning of every step (P_dep = 1 - P_end per
@@ -88,7 +88,11 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
     integrator="rk4": n_steps fixed steps of ds; "adaptive": the reference's
     solve() -- Tsit5 with DiffEq's step control (abstol, reltol, dtmax = ds) over
     n_chunks tspans covering s_max from s0; n_steps is then the accepted-step
-    capacity per ray (status MAX_STEPS when exceeded)."""
+    capacity per ray (status MAX_STEPS when exceeded).
+
+    n_gpus: None traces on the plasma's device (torj_trace_ex); an integer runs
+    make_beam's multi-GPU path (torj_trace_beam): n_shards contiguous shards
+    (0: one per GPU) over n_gpus devices, dP_shell summed by an RCCL all-reduce."""
     xs, Ns = soa(x0), soa(N0)
     n = xs.shape[1]
     if chunk_steps is None:
@@ -111,9 +115,13 @@ def trace(plasma, x0, N0, omega: float, mode: int, *, ds: float = 1e-4, n_steps:
     Pdep = np.zeros(n)
     n_save = n_steps // traj_stride if traj_stride > 0 else 0
     traj = np.zeros((n_save, 5, n)) if n_save > 0 else None
-    check(lib().torj_trace_ex(plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi,
-                              dptr(g) if n_psi else None, dptr(xl), dptr(sv), dptr(state),
-                              iptr(status), iptr(steps), dptr(dP), dptr(Pdep), dptr(traj)))
+    args = (plasma.handle, cfg, n, dptr(xs), dptr(Ns), dptr(w), n_psi, dptr(g) if n_psi else None,
+            dptr(xl), dptr(sv), dptr(state), iptr(status), iptr(steps), dptr(dP), dptr(Pdep),
+            dptr(traj))
+    if n_gpus is None:
+        check(lib().torj_trace_ex(*args))
+    else:
+        check(lib().torj_trace_beam(*args, int(n_gpus), int(n_shards)))
     return TraceResult(state.T.copy(), status, steps, dP, Pdep,
                        traj.transpose(2, 0, 1).copy() if traj is not None else None)
 
@@ -155,13 +163,26 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
     return s, u, P_beam, dP_dV, float(r.P_dep[0])
 
 
+def _final_arc_length(res, i, s0, ds, integrator):
+    """Arc length of ray i's final state: s0 + steps * ds for RK4 (the kernel's
+    own fma), not recorded for the adaptive integrator's unsaved last step."""
+    if integrator == "rk4":
+        return s0 + ds * int(res.steps[i])
+    raise ValueError("make_beam: traj_stride must divide the step count with integrator='adaptive'")
+
+
 def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
               steering_angle_pol: float, spot_size: float, inverse_curvature_radius: float,
               f: float, mode: int, s_max: float, psi_dP_dV, *, ds: float = 1e-4,
               traj_stride: int = 1, deposition: str = "reference", integrator: str = "rk4",
-              max_steps: int | None = None, absorption="albajar", **kwargs):
+              max_steps: int | None = None, absorption="albajar", n_gpus: int = 1, **kwargs):
     """make_beam (src/solve.jl:209-242) -> (arc_lengths, trajectories, ray_powers, dP_dV,
-    deposited_power, ray_weights).  kwargs go to launch_peripheral_rays."""
+    deposited_power, ray_weights).  kwargs go to launch_peripheral_rays.  The rays
+    are traced by torj_trace_beam over n_gpus devices of this process (the
+    reference's per-ray Dagger tasks, src/solve.jl:219-224) and their deposition
+    summed across them (:233-240).  traj_stride > 1 keeps every traj_stride-th
+    step of each ray plus its final state, so ray_powers[i][-1] is the ray's
+    final P as in the reference."""
     omega = 2.0 * np.pi * f
     N0 = pol_tor_angles_2_vector(steering_angle_pol, steering_angle_tor)
     x0 = np.array([r * np.cos(phi), r * np.sin(phi), z])
@@ -177,7 +198,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     g = f64(psi_dP_dV)
     res = trace(plasma, xp, Np, omega, mode, ds=ds, n_steps=n_steps, psi_grid=g, weights=w,
                 traj_stride=traj_stride, deposition=deposition, x_launch=pos, s0=s0,
-                integrator=integrator, s_max=s_max, absorption=absorption)
+                integrator=integrator, s_max=s_max, absorption=absorption, n_gpus=n_gpus)
     if (res.status == MAX_STEPS).any():
         raise RuntimeError("make_beam: accepted-step capacity exhausted (raise max_steps)")
     dV = plasma.shell_volumes(g)
@@ -187,7 +208,13 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     arc_lengths, trajectories, ray_powers = [], [], []
     for i in range(len(w)):
         k = int(res.steps[i]) // traj_stride
-        arc_lengths.append(np.concatenate([[0.0, s0[i]], res.traj[i, :k, 4]]))
-        trajectories.append(np.vstack([pos[i][None], xp[i][None], res.traj[i, :k, :3]]))
-        ray_powers.append(np.concatenate([[1.0, 1.0], np.exp(-res.traj[i, :k, 3])]))
+        s_i, x_i, tau_i = res.traj[i, :k, 4], res.traj[i, :k, :3], res.traj[i, :k, 3]
+        if int(res.steps[i]) % traj_stride:  # the final state is not a saved sample
+            s_end = _final_arc_length(res, i, s0[i], ds, integrator)
+            s_i = np.concatenate([s_i, [s_end]])
+            x_i = np.vstack([x_i, res.state[i, :3][None]])
+            tau_i = np.concatenate([tau_i, [res.state[i, 6]]])
+        arc_lengths.append(np.concatenate([[0.0, s0[i]], s_i]))
+        trajectories.append(np.vstack([pos[i][None], xp[i][None], x_i]))
+        ray_powers.append(np.concatenate([[1.0, 1.0], np.exp(-tau_i)]))
     return arc_lengths, trajectories, ray_powers, dP_dV, deposited_power, w
