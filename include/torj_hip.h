@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 2
+#define TORJ_ABI_VERSION 3  /* 3: torj_trace_beam, sticky launch flags */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {

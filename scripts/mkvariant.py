@@ -21,5 +21,5 @@ for spec in specs:
 out = os.path.join(ROOT, "torj.jl_amd", "build", "variants", f"libtorj_hip_{name}.so")
 os.makedirs(os.path.dirname(out), exist_ok=True)
 subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC",
-                       "-fopenmp", "-shared", "-o", out, "torj_hip.hip"], cwd=f"{base}/pkg/csrc")
+                       "-fopenmp", "-shared", "-o", out, "torj_hip.hip", "-L/opt/rocm/lib", "-lrccl"], cwd=f"{base}/pkg/csrc")
 print(out)

@@ -3,13 +3,15 @@
 //   warm_check host        host build only: alpha_warm / dieltens_* over a seeded
 //                          point set, for running under -fsanitize=address,undefined
 //                          (tests/native/Makefile target warm_check_asan)
-//   warm_check gpu         the same points on the device through three entry
-//                          shapes -- alpha_warm inlined into the kernel (what the
-//                          trace kernels do), alpha_warm behind a noinline call
-//                          (DESIGN.md 3.6's formerly wrong variant) and the fully
-//                          relativistic tensor behind a noinline call -- each
-//                          compared with the host build; prints the worst
-//                          relative difference per variant and exits 1 above 1e-9.
+//   warm_check gpu         the same points on the device: alpha (by value, as the
+//                          library's kernels call it) inlined into the kernel and
+//                          behind a noinline call, against the host build and each
+//                          other (exit 1 above 1e-9); and the toolchain
+//                          reproducer of DESIGN.md 3.6 -- the fully relativistic
+//                          tensor behind a noinline call, from a kernel without and
+//                          with a private frame of its own (reported, not graded:
+//                          with a caller frame the callee's local arrays read back
+//                          as zeros under ROCm 7.2 / gfx950).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -34,11 +36,19 @@ struct Pt {
     int mode, iwarm;
 };
 
-__device__ __attribute__((noinline)) double alpha_warm_noinline(double om, double X, double Y,
-                                                               double Na, double Np, double Te,
-                                                               double inv, int mode, int iwarm,
-                                                               cplx *n2) {
-    return alpha_warm(om, X, Y, Na, Np, Te, inv, mode, iwarm, n2);
+// Out of line: in the default build a noinline wrapper around the inlined
+// alpha_warm_v; in the WC_NI build (TORJ_WARM_ATTR noinline) alpha_warm_v is
+// itself the out-of-line function, called straight from the kernel -- a
+// wrapper there would give alpha_warm_v a caller frame, the trigger above.
+#if WC_NI
+__device__ __forceinline__
+#else
+__device__ __attribute__((noinline))
+#endif
+WarmAlpha alpha_warm_noinline(double om, double X, double Y, double Na, double Np, double Te,
+                              double inv, int mode, int iwarm) {
+    return iwarm == 1 ? alpha_warm_v<1>(om, X, Y, Na, Np, Te, inv, mode)
+                      : alpha_warm_v<3>(om, X, Y, Na, Np, Te, inv, mode);
 }
 
 __device__ __attribute__((noinline)) void dieltens_fr_noinline(double X, double Y, double Np,
@@ -47,17 +57,19 @@ __device__ __attribute__((noinline)) void dieltens_fr_noinline(double X, double 
     dieltens_fr<kWarmMaxL>(X, Y, Np, mu, lrm, *T);
 }
 
+// the API shape the library's kernels use: alpha and N_perp^2 by value, no
+// private frame in the kernel
 __global__ void WC_LB k_alpha(const Pt *p, int n, int variant, double *out) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const Pt q = p[i];
-    cplx n2 = C(0.0);
-    double a;
+    WarmAlpha r;
     if (variant == 0)
-        a = alpha_warm(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm, &n2);
+        r = q.iwarm == 1 ? alpha_warm_v<1>(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode)
+                         : alpha_warm_v<3>(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode);
     else
-        a = alpha_warm_noinline(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm, &n2);
-    out[3 * i] = a, out[3 * i + 1] = n2.re, out[3 * i + 2] = n2.im;
+        r = alpha_warm_noinline(q.om, q.X, q.Y, q.Nabs, q.Npar, q.Te, q.inv, q.mode, q.iwarm);
+    out[3 * i] = r.alpha, out[3 * i + 1] = r.n2.re, out[3 * i + 2] = r.n2.im;
 }
 
 __global__ void WC_LB k_tensor_fr(const Pt *p, int n, Tensor<kWarmMaxL> *out) {
@@ -71,6 +83,39 @@ __global__ void WC_LB k_tensor_fr(const Pt *p, int n, Tensor<kWarmMaxL> *out) {
         for (int c = 0; c < 6; c++) T.e[l][c] = C(0.0);
     dieltens_fr_noinline(q.X, q.Y, q.Npar, mu, lrm, &T);
     out[i] = T;
+}
+
+// the same call with 256 more bytes of kernel frame below the tensor
+__global__ void WC_LB k_tensor_fr_pad(const Pt *p, int n, Tensor<kWarmMaxL> *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Pt q = p[i];
+    const double mu = kMe * kC * kC / (q.Te * kE);
+    const int lrm = std::min(larmornumber(q.Y, q.Npar, mu), kWarmMaxL);
+    volatile double pad[32];
+    for (int k = 0; k < 32; k++) pad[k] = k;
+    Tensor<kWarmMaxL> T;
+    for (int l = 0; l < kWarmMaxL; l++)
+        for (int c = 0; c < 6; c++) T.e[l][c] = C(0.0);
+    dieltens_fr_noinline(q.X, q.Y, q.Npar, mu, lrm, &T);
+    out[i] = T;
+    out[i].e330.im += pad[q.mode > 2 ? 1 : 0] * 0.0;
+}
+
+// tensor in global memory, but the kernel keeps a small private frame of its
+// own, so the callee's frame starts at a non-zero stack offset
+__global__ void WC_LB k_tensor_fr_global_pad(const Pt *p, int n, Tensor<kWarmMaxL> *out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const Pt q = p[i];
+    const double mu = kMe * kC * kC / (q.Te * kE);
+    const int lrm = std::min(larmornumber(q.Y, q.Npar, mu), kWarmMaxL);
+    volatile double pad[32];
+    for (int k = 0; k < 32; k++) pad[k] = k;
+    for (int l = 0; l < kWarmMaxL; l++)
+        for (int c = 0; c < 6; c++) out[i].e[l][c] = C(0.0);
+    dieltens_fr_noinline(q.X, q.Y, q.Npar, mu, lrm, &out[i]);
+    out[i].e330.im += pad[q.mode > 2 ? 1 : 0] * 0.0;
 }
 
 // the same noinline tensor call writing straight into global memory (no
@@ -186,9 +231,14 @@ int main(int argc, char **argv) {
     printf("inlined vs noinline: %d of %d outputs differ, max rel %.3e\n", ndiff, 3 * m, ed);
     if (ed > 1e-9) bad = 1;
     std::vector<Tensor<kWarmMaxL>> gT(m);
-  for (int tv = 0; tv < 2; tv++) {
-    if (tv == 0)
+  // tv 0, 2: the toolchain reproducer -- reported, not graded
+  for (int tv = 0; tv < 4; tv++) {
+    if (tv == 3)
+        hipLaunchKernelGGL(k_tensor_fr_global_pad, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, dT);
+    else if (tv == 0)
         hipLaunchKernelGGL(k_tensor_fr, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, dT);
+    else if (tv == 2)
+        hipLaunchKernelGGL(k_tensor_fr_pad, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, dT);
     else
         hipLaunchKernelGGL(k_tensor_fr_global, dim3((m + 63) / 64), dim3(64), 0, 0, dP, m, dT);
     if (hipDeviceSynchronize() || hipMemcpy(gT.data(), dT, m * sizeof(Tensor<kWarmMaxL>), hipMemcpyDeviceToHost))
@@ -207,9 +257,12 @@ int main(int argc, char **argv) {
             }
     }
     printf("%s: max diff / tensor scale %.3e (point %d, l %d, c %d: dev (%.6e, %.6e) host (%.6e, %.6e))\n",
-           tv ? "dieltens_fr noinline, tensor in global memory" : "dieltens_fr noinline, tensor in the kernel frame",
+           tv == 3 ? "[toolchain reproducer] dieltens_fr noinline, tensor in global memory, kernel with a frame"
+           : tv == 1 ? "dieltens_fr noinline, tensor in global memory"
+           : tv == 0 ? "[toolchain reproducer] dieltens_fr noinline, tensor in the kernel frame"
+                     : "[toolchain reproducer] dieltens_fr noinline, tensor in a 256-B-larger kernel frame",
            et, wt, wl + 1, wc, gT[wt].e[wl][wc].re, gT[wt].e[wl][wc].im, hT[wt].e[wl][wc].re, hT[wt].e[wl][wc].im);
-    if (et > 1e-9) bad = 1;
+    if (tv == 1 && et > 1e-9) bad = 1;
   }
     printf(bad ? "FAIL\n" : "OK\n");
     return bad;

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(T):
 
 
 def test_abi_version_and_errors(T):
-    assert T.lib().torj_abi_version() == 2
+    assert T.lib().torj_abi_version() == T._lib.ABI_VERSION == 3
     with pytest.raises(ValueError, match="N_rings"):
         T.launch_peripheral_rays([0, 0, 0], [0, 0, 1.0], 0.0174, 1 / 3.99, 92.5e9, N_rings=1)
     with pytest.raises(T.TorjError, match="abs_Al_init"):
@@ -53,6 +53,32 @@ def test_plasma_from_coefs_roundtrip(T, hplasma, eq):
                              np.zeros(len(eq["eqt1d_psi_norm"]) + 2), hplasma.psi_prof_max)
     for k in c:
         assert np.array_equal(P2.coefs(k), c[k])
+
+
+def test_plasma_from_interpolations_layout_coefs(T, hplasma, oplasma, eq):
+    """The Julia shim's GPUPlasma(::TorJ.Plasma) path: a handle built from
+    Interpolations.jl-layout coefficient arrays ((nR+2, nZ+2), column-major,
+    parent(spl.itp.itp.coefs)) -- here the oracle's own prefilter output (dense
+    LU, independent of the product's Thomas solve) and its volume spline -- gives
+    the ray entry (host path: bisection on psi + refraction) of the handle built
+    from the raw maps."""
+    oc = oplasma.field_coefs()
+    v = oplasma.s.vol
+    vol = np.ctypeslib.as_array(v.coef, shape=(v.n + 2,)).copy()
+    P2 = T.Plasma.from_coefs((eq["R_coords"][0], eq["R_coords"][-1]),
+                             (eq["Z_coords"][0], eq["Z_coords"][-1]), oc, (v.x1, v.xn), vol,
+                             oplasma.psi_prof_max)
+    for p in (0.0, 0.3, 0.77, 1.0):
+        assert abs(P2.volume(p) - hplasma.volume(p)) < 1e-12
+    om = 2 * np.pi * 92.5e9
+    N0 = T.pol_tor_angles_2_vector(np.deg2rad(30), 0.0)
+    pos, dirs, w = T.launch_peripheral_rays([2.5, 0, 0.4], N0, 0.0174, 1 / 3.99, 92.5e9,
+                                            N_rings=4, min_azimuthal_points=5)
+    a = T.ray_entry(hplasma, pos, dirs, om, 1)
+    b = T.ray_entry(P2, pos, dirs, om, 1)
+    assert np.array_equal(a[3], b[3]) and (a[3] == 0).all()
+    for u, q in zip(a[:3], b[:3]):
+        assert np.abs(u - q).max() < 1e-11
 
 
 def test_launch_fan_matches_oracle(T, O):

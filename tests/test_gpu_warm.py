@@ -123,3 +123,25 @@ def test_warm_deposition_conserves_power(gpu, T, hplasma):
     assert tot > 0.5 * w.sum()
     assert abs(r.dP_shell[:-1].sum() - tot) <= 1e-12 * tot
     assert abs(r.dP_shell[-1] - tot) <= 1e-12 * tot
+
+
+def test_warm_alpha_inlined_and_out_of_line_builds(gpu):
+    """The warm alpha as the library's kernels call it (alpha and N_perp^2 by
+    value) inlined into the kernel and behind a noinline call
+    (TORJ_WARM_ATTR), on 4 001 points vs the host build of the same source
+    (tests/native/warm_check.hip, built by __graft_entry__.build()).  The
+    harness also prints its toolchain reproducer: a noinline
+    callee with a large frame called from a kernel with a private frame of
+    its own reads its own local arrays back as zeros; that case is reported,
+    not graded."""
+    import os
+    import subprocess
+
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native", "build")
+    for exe in ("warm_check", "warm_check_ni"):
+        path = os.path.join(here, exe)
+        assert os.path.exists(path), f"{path} missing: run __graft_entry__.build()"
+        r = subprocess.run([path, "gpu", "4000"], capture_output=True, text=True, timeout=180)
+        print(r.stdout)
+        assert r.returncode == 0, (exe, r.stdout[-2000:], r.stderr[-2000:])
+        assert "inlined vs noinline: 0 of" in r.stdout

@@ -739,18 +739,30 @@ TORJ_HD int larmornumber(double yg, double npl, double mu) {
 
 // alpha (:1328-1337): iwarm 1 (weakly relativistic) or 3 (fully relativistic,
 // the reference's choice); inv_dDdN = 1 / |dD/dN| (R4); sox from mode (R5).
-// Returns alpha [1/m]; N_perp^2 (warm) in *n2 if given.
-// Inlined into its callers.  A noinline device build (ROCm 7.2, gfx950; -O3
-// and -O1 alike) returned the anti-hermitian part ~1e-10 of its value for some
-// inputs while the same source is exact on the host and when inlined, and a
-// printf inside the loop made it exact again: codegen-dependent, not isolated
-// further.  tests/test_gpu_warm.py pins the device result to the oracle.
+// Returns alpha [1/m] and N_perp^2 (warm) by value.
+//
+// No pointer into a caller's private (scratch) frame crosses a call here:
+// with this ROCm 7.2 gfx950 toolchain, a non-inlined function that receives a
+// flat pointer to its caller's stack frame, as alpha_warm_t's former
+// `cplx *n2` out-argument and dieltens_fr(..., Tensor &T) behind a noinline
+// call did, read its OWN local arrays back wrong (the fully relativistic
+// tensor's anti-hermitian part came out 0 or ~1e-10 of its value) once the
+// caller had a frame of its own -- the same callee was exact when the pointer
+// went to global memory, or the caller had no frame (tests/native/
+// warm_check.hip reproduces it: "tensor in the kernel frame" vs "tensor in
+// global memory").  A printf changed the frame layout and hid
+// it.  The warm kernels inline this code; the out-of-line build
+// (TORJ_WARM_ATTR noinline) returns by value and is pinned by the same tests.
 #ifndef TORJ_WARM_ATTR
 #define TORJ_WARM_ATTR TORJ_HD
 #endif
+struct WarmAlpha {
+    double alpha;
+    cplx n2;
+};
 template <int IWARM, int L>
-TORJ_HD double alpha_core(double omega, double X, double Y, double N_par, double mu, double npr,
-                          int lrm, double inv_dDdN, int mode, cplx *n2) {
+TORJ_HD WarmAlpha alpha_core(double omega, double X, double Y, double N_par, double mu, double npr,
+                             int lrm, double inv_dDdN, int mode) {
     Tensor<L> T;
     if constexpr (IWARM == 1)
         dieltens_wr<L>(X, Y, N_par, mu, lrm, T);
@@ -761,16 +773,15 @@ TORJ_HD double alpha_core(double omega, double X, double Y, double N_par, double
     T.e[0][2] = T.e[0][2] + 1.0;
     const int sox = Y <= 1.0 ? mode : -mode;
     const cplx a2 = warmdisp_n2<L>(X, Y, N_par, npr, sox, lrm, T);
-    if (n2) *n2 = a2;
-    return 2.0 * a2.im * omega / kC * inv_dDdN;
+    return {2.0 * a2.im * omega / kC * inv_dDdN, a2};
 }
 
 // The tensor is sized for lrm <= 3 (the common case: one to three Larmor
 // orders up to the third harmonic) or lrm <= 5; on the device the choice is
 // made per wave (ballot), so the heavy code never diverges between the two.
 template <int IWARM>
-TORJ_WARM_ATTR double alpha_warm_t(double omega, double X, double Y, double N_abs, double N_par,
-                                   double Te, double inv_dDdN, int mode, cplx *n2) {
+TORJ_WARM_ATTR WarmAlpha alpha_warm_v(double omega, double X, double Y, double N_abs, double N_par,
+                                      double Te, double inv_dDdN, int mode) {
     const double mu = kMe * kC * kC / (Te * kE);
     const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
     const int nharm = larmornumber(Y, N_par, mu);
@@ -780,8 +791,16 @@ TORJ_WARM_ATTR double alpha_warm_t(double omega, double X, double Y, double N_ab
 #else
     const bool big = lrm > 3;
 #endif
-    return big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode, n2)
-               : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode, n2);
+    return big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode)
+               : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode);
+}
+
+template <int IWARM>
+TORJ_HD double alpha_warm_t(double omega, double X, double Y, double N_abs, double N_par,
+                            double Te, double inv_dDdN, int mode, cplx *n2) {
+    const WarmAlpha r = alpha_warm_v<IWARM>(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode);
+    if (n2) *n2 = r.n2;
+    return r.alpha;
 }
 
 // runtime iwarm (1 or 3): the point entry torj_alpha_warm and the host tests

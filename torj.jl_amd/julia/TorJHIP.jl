@@ -5,14 +5,26 @@
 # Usage (see INTEGRATION.md):
 #     using TorJ, TorJHIP
 #     TorJHIP.abs_Al_init(24)
-#     gp = TorJHIP.GPUPlasma(R, Z, psi_norm, psi_prof, ne, Te, Br, Bz, Bphi, eq_psi, eq_vol)
-#     s, u, P, dP_dV, P_dep = TorJHIP.make_ray(gp, x0, N0, f, 1, 0.4, psi_dP_dV)
+#     plasma = TorJ.Plasma(R, Z, psi_norm, psi_prof, ne, Te, Br, Bz, Bphi, eq_psi, eq_vol)
+#     s, u, P, dP_dV, P_dep = TorJHIP.make_ray(plasma, x0, N0, f, 1, 0.4, psi_dP_dV)
+#     out = TorJHIP.make_beam(plasma, r, phi, z, tor, pol, spot, inv_curv, f, 1, 1.0,
+#                             psi_dP_dV; N_rings=92, min_azimuthal_points=11, n_gpus=8)
+# A TorJ.Plasma is converted once (GPUPlasma(plasma): its Interpolations.jl
+# B-spline coefficients go to the GPU as they are) and cached per object.
 #
 # Untested in this repository's container (no Julia toolchain); the same ABI is
 # exercised by the Python ctypes mirror in torj.jl_amd/torj_hip.
 module TorJHIP
 
+import TorJ
+
 const libtorj = get(ENV, "TORJ_HIP_LIB", joinpath(@__DIR__, "..", "build", "libtorj_hip.so"))
+const ABI_VERSION = 3  # include/torj_hip.h TORJ_ABI_VERSION
+
+function __init__()
+    v = ccall((:torj_abi_version, libtorj), Cint, ())
+    v == ABI_VERSION || error("libtorj_hip.so at $libtorj has ABI version $v, TorJHIP expects $ABI_VERSION")
+end
 
 struct TraceCfg              # torj_trace_cfg
     omega::Float64
@@ -40,23 +52,64 @@ abs_Al_init(n::Integer) = check(ccall((:torj_abs_al_init, libtorj), Cint, (Cint,
 mutable struct GPUPlasma
     h::Ptr{Cvoid}
     psi_prof_max::Float64
-    function GPUPlasma(R::Vector{Float64}, Z::Vector{Float64}, psi_norm::Matrix{Float64},
-                       psi_prof::Vector{Float64}, ne::Vector{Float64}, Te::Vector{Float64},
-                       Br::Matrix{Float64}, Bz::Matrix{Float64}, Bphi::Matrix{Float64},
-                       eq_psi::Vector{Float64}, eq_vol::Vector{Float64}; device::Integer=0)
-        h = Ref{Ptr{Cvoid}}(C_NULL)
-        # Julia matrices are (nR, nZ) column-major: exactly the ABI layout
-        check(ccall((:torj_plasma_create, libtorj), Cint,
-                    (Cint, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Float64},
-                     Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint,
-                     Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Ptr{Cvoid}}),
-                    length(R), length(Z), R, Z, psi_norm, length(psi_prof), psi_prof, ne, Te,
-                    Br, Bz, Bphi, length(eq_psi), eq_psi, eq_vol, device, h))
-        p = new(h[], maximum(psi_prof))
+    function GPUPlasma(h::Ptr{Cvoid}, psi_prof_max::Float64)
+        p = new(h, psi_prof_max)
         finalizer(x -> ccall((:torj_plasma_destroy, libtorj), Cint, (Ptr{Cvoid},), x.h), p)
         return p
     end
 end
+
+"""GPUPlasma from the raw maps -- the arguments of TorJ.Plasma (src/plasma.jl:30-32);
+the B-spline prefilter runs in the library."""
+function GPUPlasma(R::Vector{Float64}, Z::Vector{Float64}, psi_norm::Matrix{Float64},
+                   psi_prof::Vector{Float64}, ne::Vector{Float64}, Te::Vector{Float64},
+                   Br::Matrix{Float64}, Bz::Matrix{Float64}, Bphi::Matrix{Float64},
+                   eq_psi::Vector{Float64}, eq_vol::Vector{Float64}; device::Integer=0)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    # Julia matrices are (nR, nZ) column-major: exactly the ABI layout
+    check(ccall((:torj_plasma_create, libtorj), Cint,
+                (Cint, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint,
+                 Ptr{Float64}, Ptr{Float64}, Cint, Ptr{Ptr{Cvoid}}),
+                length(R), length(Z), R, Z, psi_norm, length(psi_prof), psi_prof, ne, Te,
+                Br, Bz, Bphi, length(eq_psi), eq_psi, eq_vol, device, h))
+    return GPUPlasma(h[], maximum(psi_prof))
+end
+
+# Interpolations.jl: cubic_spline_interpolation(ranges, A; extrapolation_bc=Line())
+# is extrapolate(scale(interpolate(A, BSpline(Cubic(Line(OnGrid())))), ranges...), Line());
+# .itp is the ScaledInterpolation (its .ranges), .itp.itp the BSplineInterpolation
+# whose padded coefficient OffsetArray has parent (n+2) x (m+2).
+_coefs(spl) = Array{Float64}(parent(spl.itp.itp.coefs))
+_ranges(spl) = spl.itp.ranges
+
+"""GPUPlasma(plasma::TorJ.Plasma) -- the TorJ object itself (src/plasma.jl:2-14): its six
+2-D splines' coefficients (psi, ln ne, ln Te, Br, Bz, Bphi) and the 1-D volume spline
+go to the GPU unchanged (torj_plasma_create_from_coefs), so the GPU evaluates exactly
+the splines TorJ built."""
+function GPUPlasma(p::TorJ.Plasma; device::Integer=0)
+    rR, rZ = _ranges(p.psi_norm_spline)
+    c = [_coefs(getfield(p, f)) for f in (:psi_norm_spline, :ne_spline, :Te_spline,
+                                           :Br_spline, :Bz_spline, :Bϕ_spline)]
+    all(size(x) == (length(rR) + 2, length(rZ) + 2) for x in c) ||
+        throw(ArgumentError("TorJ.Plasma splines are not on one (R, Z) grid"))
+    rv = _ranges(p.volume_psi_spline)[1]
+    cv = _coefs(p.volume_psi_spline)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:torj_plasma_create_from_coefs, libtorj), Cint,
+                (Cint, Cint, Float64, Float64, Float64, Float64, Ptr{Float64}, Ptr{Float64},
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint, Float64, Float64,
+                 Ptr{Float64}, Float64, Cint, Ptr{Ptr{Cvoid}}),
+                length(rR), length(rZ), first(rR), last(rR), first(rZ), last(rZ), c[1], c[2],
+                c[3], c[4], c[5], c[6], length(rv), first(rv), last(rv), cv,
+                Float64(p.psi_prof_max), device, h))
+    return GPUPlasma(h[], Float64(p.psi_prof_max))
+end
+
+# one GPU copy per TorJ.Plasma object (make_ray / make_beam on TorJ's own type)
+const _gpu_cache = IdDict{Any,GPUPlasma}()
+const _gpu_lock = ReentrantLock()
+gpu_plasma(p::TorJ.Plasma) = lock(() -> get!(() -> GPUPlasma(p), _gpu_cache, p), _gpu_lock)
 
 """first_point + vacuum_plasma_refraction for n rays (x0, N0: n x 3), on the GPU."""
 function ray_entry(p::GPUPlasma, x0::Matrix{Float64}, N0::Matrix{Float64}, omega, mode)
@@ -71,18 +124,20 @@ end
 
 function trace(p::GPUPlasma, cfg::TraceCfg, x0::Matrix{Float64}, N0::Matrix{Float64},
                w::Vector{Float64}, psi_grid::Vector{Float64}, x_launch::Matrix{Float64},
-               s0::Vector{Float64})
+               s0::Vector{Float64}; n_gpus::Integer=1, n_shards::Integer=0)
     n = size(x0, 1)
     n_save = cfg.traj_stride > 0 ? cfg.n_steps ÷ cfg.traj_stride : 0
     state, status, steps = zeros(n, 7), zeros(Cint, n), zeros(Cint, n)
-    dP, Pdep, traj = zeros(length(psi_grid) + 1), zeros(n), zeros(n, 5, max(n_save, 1))
+    dP, Pdep = zeros(length(psi_grid) + 1), zeros(n)
+    traj = n_save > 0 ? zeros(n, 5, n_save) : zeros(0, 5, 0)
     GC.@preserve x0 N0 w psi_grid x_launch s0 begin
-        check(ccall((:torj_trace_ex, libtorj), Cint,
+        # make_beam's fan-out over n_gpus devices + the RCCL reduce of dP_shell
+        check(ccall((:torj_trace_beam, libtorj), Cint,
                     (Ptr{Cvoid}, Ref{TraceCfg}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
                      Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Cint},
-                     Ptr{Cint}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                     Ptr{Cint}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint, Cint),
                     p.h, cfg, n, x0, N0, w, length(psi_grid), psi_grid, x_launch, s0, state,
-                    status, steps, dP, Pdep, n_save > 0 ? traj : C_NULL))
+                    status, steps, dP, Pdep, n_save > 0 ? traj : C_NULL, n_gpus, n_shards))
     end
     return state, status, steps, dP, Pdep, traj
 end
@@ -117,14 +172,18 @@ function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f:
     dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, g)
     return s, u, P_beam, dP_dV, Pdep[1]
 end
+make_ray(p::TorJ.Plasma, args...; kw...) = make_ray(gpu_plasma(p), args...; kw...)
 
 """make_beam -- same signature and return tuple as TorJ.make_beam (src/solve.jl:209-242);
-uses TorJ.launch_peripheral_rays / IMAS angles on the host, the GPU for every ray."""
+the launch fan and IMAS angles on the host, every ray on the GPU(s): n_gpus devices of
+this process (torj_trace_beam), dP_shell summed across them by RCCL.  traj_stride keeps
+every traj_stride-th step of each ray (1 = all, as the reference) plus its final state."""
 function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::Integer,
                    s_max::Float64, psi_dP_dV::Vector{Float64}; ds::Float64=1e-4,
                    N_rings::Integer=3, min_azimuthal_points::Integer=5,
                    normalize_weight_sum::Bool=true, deposition::Integer=1,
-                   integrator::Integer=0, absorption::Integer=1)
+                   integrator::Integer=0, absorption::Integer=1, traj_stride::Integer=1,
+                   n_gpus::Integer=1)
     N0 = zeros(3)
     ccall((:torj_pol_tor_angles_2_vector, libtorj), Cvoid, (Float64, Float64, Ptr{Float64}),
           pol, tor, N0)
@@ -147,16 +206,28 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     all(st .== 0) || throw(AssertionError("ray entry failed for $(count(st .!= 0)) rays"))
     n_steps = max(1, round(Int, s_max / ds))
     cap = integrator == 1 ? 2n_steps + 400 : n_steps
-    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, absorption, 1, deposition,
-                   integrator, 1e-6, 1e-6, s_max, 100)
-    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0)
+    traj_stride >= 1 || throw(ArgumentError("traj_stride must be >= 1"))
+    cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, absorption, traj_stride,
+                   deposition, integrator, 1e-6, 1e-6, s_max, 100)
+    state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0;
+                                                 n_gpus=n_gpus)
     dP_dV = zeros(length(psi_dP_dV))
     dP_dV[1:end-1] .= dP[1:end-2] ./ shell_volumes(p, psi_dP_dV)
-    arc_lengths = [vcat(0.0, s0[i], traj[i, 5, 1:steps[i]]) for i in 1:n]
-    trajectories = [vcat([pos[i, :]], [xp[i, :]], [traj[i, 1:3, k] for k in 1:steps[i]]) for i in 1:n]
-    ray_powers = [vcat(1.0, 1.0, exp.(-traj[i, 4, 1:steps[i]])) for i in 1:n]
+    arc_lengths, trajectories, ray_powers = Vector{Vector{Float64}}(), Vector{Vector{Vector{Float64}}}(), Vector{Vector{Float64}}()
+    for i in 1:n
+        k = steps[i] ÷ traj_stride
+        s_i, x_i, τ_i = traj[i, 5, 1:k], [traj[i, 1:3, j] for j in 1:k], traj[i, 4, 1:k]
+        if steps[i] % traj_stride != 0  # the final state is not a saved sample
+            integrator == 0 || throw(ArgumentError("traj_stride must divide the step count (adaptive)"))
+            push!(s_i, s0[i] + ds * steps[i]); push!(x_i, state[i, 1:3]); push!(τ_i, state[i, 7])
+        end
+        push!(arc_lengths, vcat(0.0, s0[i], s_i))
+        push!(trajectories, vcat([pos[i, :]], [xp[i, :]], x_i))
+        push!(ray_powers, vcat(1.0, 1.0, exp.(-τ_i)))
+    end
     return arc_lengths, trajectories, ray_powers, dP_dV, dP[end], w
 end
+make_beam(p::TorJ.Plasma, args...; kw...) = make_beam(gpu_plasma(p), args...; kw...)
 
 """alpha(...) of src/general_absorption.jl:1328-1337 (repaired, DESIGN.md §3.6) at n
 points on the GPU: iwarm 1 (weakly) or 3 (fully relativistic); inv_dDdN = 1/|dD/dN|.

@@ -92,6 +92,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
+ABI_VERSION = 3  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 
@@ -113,6 +114,9 @@ def lib():
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args
+        v = L.torj_abi_version()
+        if v != ABI_VERSION:
+            raise TorjError(f"{LIB_PATH} has ABI version {v}, this mirror expects {ABI_VERSION}")
         _lib = L
     return _lib
 
