@@ -131,7 +131,7 @@ def main():
     cap = 2 * args.n_steps + 400 if adaptive else args.n_steps  # accepted-step capacity
     n_save = (cap if adaptive else args.n_steps) // args.traj_stride if args.traj_stride > 0 else 0
     d_traj = torch.empty((max(n_save, 1), 5, n), dtype=torch.float64, device=dev)
-    d_cnt = torch.zeros(5, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(6, dtype=torch.int64, device=dev)
     dep = 1 if args.deposition == "reference" else 0
     cfg = T._lib.TraceCfg(omega, args.mode, args.ds, cap, max(1, args.n_steps // 100),
                           1.0, 1e-6, ABSORPTION[args.absorption], args.traj_stride, dep,
@@ -289,7 +289,8 @@ def main():
             },
             "work_counters": {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
                               "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
-                              "bessel_series_terms": int(cnt[4])},
+                              "bessel_series_terms": int(cnt[4]),
+                              "harmonic_integrals_exact_zero": int(cnt[5])},
         }
         if world == 1:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,

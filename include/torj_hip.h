@@ -207,9 +207,10 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
 
 /* Device-pointer form (inputs resident in HBM; what bench.py times).
  * dP_shell (n_psi+1) is ACCUMULATED into (zero it first).  counters (may be
- * NULL): 5 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
- * reaching the harmonic sum, harmonic integrals, Bessel-series terms -- the
- * basis of the algorithmic FLOP count.  stream: hipStream_t or NULL. */
+ * NULL): 6 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
+ * reaching the harmonic sum, harmonic integrals evaluated, Bessel-series terms,
+ * harmonic integrals found exactly zero without their node loop -- the basis
+ * of the algorithmic FLOP count.  stream: hipStream_t or NULL. */
 int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                       const double *N0, const double *weights, int n_psi,
                       const double *psi_grid, double *state, int *status, int *steps,
@@ -250,8 +251,14 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
  * trace with 16 lanes per ray (Albajar absorption, no binning: the node pairs
  * of the absorption integral split between a ray's lanes, results equal to
  * rounding; mode -1 picks it for beams of at most 2 x 64 x SIMDs / 16 rays
- * unless env TORJ_LPR=1).
- * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16)). */
+ * unless env TORJ_LPR=1); 3: the split RK4 path (fixed steps, Albajar): the
+ * trajectories' cold RK4 in one kernel, the 4 x n_steps alpha evaluations per
+ * ray in a fully parallel one, the optical depth by an in-order scan, blocks of
+ * steps pipelined over two streams (mode -1 picks it where it
+ * would pick 1, unless env TORJ_SPLIT=0).
+ * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16));
+ * steps per pipeline block for mode 3 (0 = from the 4 GiB alpha-input budget,
+ * env TORJ_SPLIT_MB). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
 /* Waits for `stream` and checks every trace launched on this handle since

@@ -1,0 +1,117 @@
+"""The split RK4 path (torj_set_sched mode 3): cold RK4
+trajectories, the alpha evaluations as a separate fully parallel kernel and the
+optical depth by an in-order scan, pipelined in blocks of steps over two
+streams.  Its outputs equal the fused one-lane kernel's to rounding (1e-12:
+the same arithmetic in separately compiled kernels, whose fma contraction may
+differ by an ulp) with identical statuses, step counts and NaN pattern; vs the
+oracle the parity bar (1e-10, statuses and steps exact)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _fan(T, hplasma, mode=1, n_rings=14, min_az=5, f=None):
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    f = f or s["f_abs_test"]
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=n_rings,
+                                            min_azimuthal_points=min_az)
+    om = 2 * np.pi * f
+    xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, mode, gpu=True)
+    assert (st == T.OK).all()
+    return pos, xp, Np, s0, w, om
+
+
+def _run(T, hplasma, sched, waves, *args, **kw):
+    try:
+        hplasma.set_sched(sched, waves)
+        return T.trace(hplasma, *args, **kw)
+    finally:
+        hplasma.set_sched(-1)
+
+
+@pytest.mark.parametrize("deposition,traj,block", [("reference", 100, 0), ("reference", 100, 60),
+                                                    ("binned", 0, 140), ("none", 7, 33)])
+def test_split_equals_fused(gpu, T, hplasma, deposition, traj, block):
+    from test_gpu_c3 import _close
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=traj)
+    if deposition != "none":
+        kw.update(psi_grid=np.linspace(0, 1, 1000), deposition=deposition, x_launch=pos, s0=s0)
+    a = _run(T, hplasma, 0, 0, xp, Np, om, 1, **kw)
+    b = _run(T, hplasma, 3, block, xp, Np, om, 1, **kw)
+    if traj == 0:
+        a.traj = b.traj = np.zeros(0)
+    if deposition == "none":
+        a.dP_shell = b.dP_shell = np.ones(1)
+    _close(a, b, 1e-12)
+
+
+def test_split_termination_vs_oracle(gpu, T, hplasma, oplasma):
+    """ABSORBED (P_min raised so rays stop mid-block at chunk boundaries),
+    LEFT_PLASMA (rays launched outwards), O-mode; with the trajectory samples
+    past a stop NaN as in the fused kernel."""
+    from test_gpu_parity import _compare_trace
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, n_rings=4)
+    x_out = np.array([[2.1, 0.0, 0.0], [1.9, 0.0, 0.3]])
+    N_out = np.array([[1.0, 0.0, 0.0], [0.2, 0.0, 1.0]])
+    for i in range(len(x_out)):
+        N_out[i] /= np.linalg.norm(N_out[i])
+        lo, hi = 0.01, 1.5
+        for _ in range(100):
+            m = 0.5 * (lo + hi)
+            d = oplasma.dispersion_relation(x_out[i], N_out[i] * m, om, 1)
+            lo, hi = (m, hi) if d < 0 else (lo, m)
+        N_out[i] *= lo
+    xp, Np = np.vstack([xp, x_out]), np.vstack([Np, N_out])
+    grid = np.linspace(0, 1, 300)
+    kw = dict(ds=1e-4, n_steps=6000, chunk_steps=60, psi_grid=grid, traj_stride=50, P_min=1e-2)
+    g = _run(T, hplasma, 3, 90, xp, Np, om, 1, **kw)
+    a = _run(T, hplasma, 0, 0, xp, Np, om, 1, **kw)
+    o = oplasma.trace(xp, Np, om, 1, 1e-4, 6000, chunk_steps=60, psi_grid=grid, traj_stride=50,
+                      P_min=1e-2)
+    _compare_trace(g, o)
+    assert T.ABSORBED in g.status.tolist() and T.LEFT_PLASMA in g.status.tolist()
+    assert np.array_equal(np.isfinite(g.traj), np.isfinite(a.traj))
+    fin = np.isfinite(a.traj)
+    assert np.abs(g.traj[fin] - a.traj[fin]).max() <= 1e-10 * np.abs(a.traj[fin]).max()
+    assert np.abs(g.dP_shell[:-1] - o["dP"]).max() <= 1e-10 * np.abs(o["dP"]).max()
+
+
+def test_split_counters_match_fused(gpu, T, hplasma):
+    """The work counters (the algorithmic FLOP count's basis) of the split path
+    equal the fused kernel's on a beam without mid-block stops."""
+    import ctypes
+    import torch
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    n = len(w)
+    dev = torch.device("cuda", 0)
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    x0, N0 = t(xp.T), t(Np.T)
+    out = []
+    for sched in (0, 3):
+        state = torch.empty((7, n), dtype=torch.float64, device=dev)
+        st = torch.empty(n, dtype=torch.int32, device=dev)
+        k = torch.empty(n, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+        cfg = T._lib.TraceCfg(om, 1, 1e-4, 1500, 15, 1.0, 1e-6, 1, 0)
+        stream = torch.cuda.current_stream(dev)
+        hplasma.set_sched(sched, 0)
+        try:
+            T._lib.check(T.lib().torj_trace_device(hplasma.handle, cfg, n, x0.data_ptr(),
+                                                   N0.data_ptr(), None, 0, None, state.data_ptr(),
+                                                   st.data_ptr(), k.data_ptr(), None, None, None,
+                                                   ctypes.c_void_p(cnt.data_ptr()),
+                                                   stream.cuda_stream))
+            T._lib.check(T.lib().torj_trace_check(hplasma.handle, stream.cuda_stream))
+        finally:
+            hplasma.set_sched(-1)
+        out.append((cnt.cpu().numpy(), state.cpu().numpy()))
+    assert np.array_equal(out[0][0], out[1][0]), (out[0][0], out[1][0])

@@ -393,12 +393,14 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
     const unsigned long long s2 = wave_sum((unsigned long long)work.n_active);
     const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
     const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
+    const unsigned long long s5 = wave_sum((unsigned long long)work.n_zero);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(a.counters + 0, s0);
         atomicAdd(a.counters + 1, s1);
         atomicAdd(a.counters + 2, s2);
         atomicAdd(a.counters + 3, s3);
         atomicAdd(a.counters + 4, s4);
+        atomicAdd(a.counters + 5, s5);
     }
 }
 
@@ -830,6 +832,378 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
 }
 
 // ---------------------------------------------------------------------------
+// Split RK4 path: trajectory and optical depth as separate, overlapped kernels
+// (fixed-step RK4, Albajar).
+//
+// In sys! (src/solve.jl:112-114) dx/ds and dN/ds are gradΛ!(x, N) alone: the
+// absorption only drives u[7].  So the trajectory of every ray is fixed before
+// any alpha is known, and the 4 x n_steps alpha evaluations of a ray are
+// independent of each other -- the step's chain is the cheap cold RHS, the
+// expensive part is embarrassingly parallel.  Per block of B steps:
+//   k_traj      one lane per ray: the cold RK4 steps (the same arithmetic as
+//               ray_segment), writing each stage's alpha inputs (X, Y, |N|,
+//               N_par, Te), psi per step, chunk-boundary states, trajectory
+//               samples; stops LEFT_PLASMA / NAN exactly as ray_segment;
+//   k_alpha_pts one lane per (ray, step, stage): abs_albajar_fast at the
+//               stored inputs -- a fully occupied grid, no step chain;
+//   k_tau_scan  one lane per ray, in step order: tau += ds/6 (a0 + 2a1 + 2a2 +
+//               a3) with ray_segment's fma order, P = exp(-tau), the ABSORBED
+//               check at chunk boundaries (after T's psi check, as the
+//               reference), make_ray's dP/ds samples, binned deposition, tau in
+//               the trajectory samples;
+// then k_split_final assembles the final state (a ray the scan stops earlier
+// than the trajectory takes its chunk-boundary state, or replays the last
+// steps when alpha itself went non-finite).  k_traj of block b+1 runs on the
+// caller's stream while k_alpha_pts / k_tau_scan of block b run on a second
+// stream: the trajectory waves (~1.5 per SIMD on a 1e5-ray beam) and the alpha
+// waves share the SIMDs.  A wave of k_alpha_pts holds the 64 rays of a 64-ray
+// group at one (step, stage): the same lanes as the fused kernel's wave there,
+// so the per-wave Bessel-level ballot and every alpha are the same bits.
+// ---------------------------------------------------------------------------
+constexpr int kAinF = 5;  // X, Y, |N|, N_par, Te
+
+struct SplitArgs {
+    double *ain;          // [j][stage][f][n]: this block's alpha inputs
+    double *alpha;        // [j][stage][n]
+    unsigned short *awork;  // [j][stage][n]: bit 0 active, bits 1-2 harmonics, 3-4 exact-zero
+                            // harmonics, 5-15 Bessel terms
+    double *psib;         // binned deposition: psi at the end of step k0 + j, [j][n]
+    double *cbx;          // [c][6][n]: x, N at chunk boundary c (steps = c * chunk_steps)
+    double *tx;           // [6][n]: the trajectory kernel's carry
+    int *tinfo;           // steps | status << 24: the trajectory kernel's stop (one store)
+    double *stau, *spsi, *sPdep;  // the scan's carry
+    int *sinfo;           // steps | status << 24: the scan's stop
+    int k0, kb;           // block: steps [k0, k0 + kb)
+};
+
+__device__ __forceinline__ int info_steps(int v) { return v & 0xffffff; }
+__device__ __forceinline__ int info_status(int v) { return (unsigned)v >> 24; }
+__device__ __forceinline__ int make_info(int steps, int st) { return steps | (st << 24); }
+
+// One cold RK4 step of ray_segment's arithmetic (plasma_point with ln Te, as
+// the absorbing kernels evaluate it); STORE: this step's alpha inputs -> ain.
+template <bool STORE>
+__device__ __forceinline__ bool cold_step(const TraceArgs &a, const SplitArgs &sp, int j, int i,
+                                          const double x[3], const double N[3], double xn[3],
+                                          double Nn[3]) {
+    const double hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
+    double acc[6] = {0, 0, 0, 0, 0, 0}, xt[3], Nt[3], k[6];
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        xt[c] = x[c];
+        Nt[c] = N[c];
+    }
+#pragma unroll 1
+    for (int st = 0; st < 4; st++) {
+        PlasmaPoint p;
+        plasma_point<true>(a.coef, a.g, a.k, xt, p);
+        double Npar, inv;
+        dispersion_grad(p, Nt, a.mode, k, &Npar, &inv);
+        if constexpr (STORE) {
+            double *o = sp.ain + ((size_t)(j * 4 + st) * kAinF) * a.n + i;
+            o[0] = p.X;
+            o[(size_t)a.n] = p.Y;
+            o[2 * (size_t)a.n] = sqrt_pos(Nt[0] * Nt[0] + Nt[1] * Nt[1] + Nt[2] * Nt[2]);
+            o[3 * (size_t)a.n] = Npar;
+            o[4 * (size_t)a.n] = exp_fast(p.lnTe);
+        }
+        const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
+        const double h = (st < 2) ? hds : a.ds;
+#pragma unroll
+        for (int c = 0; c < 6; c++) acc[c] = fma(wgt, k[c], acc[c]);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            xt[c] = fma(h, k[c], x[c]);
+            Nt[c] = fma(h, k[3 + c], N[c]);
+        }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        xn[c] = x[c] + ds6 * acc[c];
+        Nn[c] = N[c] + ds6 * acc[3 + c];
+        bad |= !isfinite(xn[c]) || !isfinite(Nn[c]);
+    }
+    return bad;
+}
+
+#ifndef TORJ_TRAJ_WAVES
+#define TORJ_TRAJ_WAVES TORJ_MIN_WAVES
+#endif
+#ifndef TORJ_ALPHA_WAVES
+#define TORJ_ALPHA_WAVES 4
+#endif
+#ifndef TORJ_ALPHA_UNROLL  // node pairs per iteration of the alpha kernel's node loop (ILP)
+#define TORJ_ALPHA_UNROLL 1
+#endif
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, SplitArgs sp) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    double x[3], N[3];
+    int steps, st;
+    if (sp.k0 == 0) {
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = a.x0[c * a.n + i];
+            N[c] = a.N0[c * a.n + i];
+            sp.cbx[c * (size_t)a.n + i] = x[c];
+            sp.cbx[(3 + c) * (size_t)a.n + i] = N[c];
+        }
+        steps = 0;
+        st = ST_OK;
+        if constexpr (DEPO != kDepoNone) {
+            const double psi0 = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+            sp.spsi[i] = psi0;  // the scan's psi_a at step 0
+            if constexpr (DEPO == kDepoSamples) {
+                a.smp_psi[smp_at(0, i, a.smp_rows)] = psi0;
+                a.smp_dpds[smp_at(0, i, a.smp_rows)] = 0.0;
+            }
+        }
+    } else {
+        const int v = sp.tinfo[i];
+        steps = info_steps(v);
+        st = info_status(v);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = sp.tx[c * (size_t)a.n + i];
+            N[c] = sp.tx[(3 + c) * (size_t)a.n + i];
+        }
+    }
+    // a ray the scan has stopped (ABSORBED) needs no more trajectory (stale reads are harmless)
+    if (st != ST_OK || (sp.k0 > 0 && info_status(sp.sinfo[i]) != ST_OK)) return;
+    const int s_end = min(a.n_steps, sp.k0 + sp.kb);
+    for (int s = steps; s < s_end; s++) {
+        double xn[3], Nn[3];
+        if (cold_step<true>(a, sp, s - sp.k0, i, x, N, xn, Nn)) {
+            st = ST_NAN;
+            break;
+        }
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = xn[c];
+            N[c] = Nn[c];
+        }
+        steps = s + 1;
+        const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
+        double psi_b = 0.0;
+        if (DEPO != kDepoNone || check)
+            psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+        if constexpr (DEPO == kDepoSamples) a.smp_psi[smp_at(steps, i, a.smp_rows)] = psi_b;
+        if constexpr (DEPO == kDepoBinned) sp.psib[(size_t)(s - sp.k0) * a.n + i] = psi_b;
+        if constexpr (TRAJ) {
+            if (a.traj_stride > 0 && (steps % a.traj_stride) == 0) {
+                double *T = a.traj + (size_t)(steps / a.traj_stride - 1) * 5 * a.n + i;
+                T[0] = x[0];
+                T[(size_t)a.n] = x[1];
+                T[2 * (size_t)a.n] = x[2];
+                T[4 * (size_t)a.n] = (a.s0 ? a.s0[i] : 0.0) + steps * a.ds;
+            }
+        }
+        if (check) {
+            double *cb = sp.cbx + (size_t)(steps / a.chunk_steps) * 6 * a.n + i;
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                cb[c * (size_t)a.n] = x[c];
+                cb[(3 + c) * (size_t)a.n] = N[c];
+            }
+            if (psi_b > a.psi_exit) {  // src/solve.jl:174
+                st = ST_LEFT_PLASMA;
+                break;
+            }
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        sp.tx[c * (size_t)a.n + i] = x[c];
+        sp.tx[(3 + c) * (size_t)a.n + i] = N[c];
+    }
+    sp.tinfo[i] = make_info(steps, st);
+}
+
+// alpha at the stored stage points of one block: block = 256 lanes = 4 groups
+// of 64 rays at one (step j, stage); lanes of rays the trajectory did not
+// reach this step with (or the scan has stopped) sit out, as in the fused wave
+// (a measured alternative -- harmonic 2 in a second pass over a compacted list
+// of the points needing it -- executed more instructions in total: the points
+// needing harmonic 2 cluster in whole waves)
+__global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
+    const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
+    const int i = q * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const int j = js >> 2;
+    const int ti = sp.tinfo[i];
+    if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
+    const double *in = sp.ain + (size_t)js * kAinF * a.n + i;
+    AlbajarWork work = {0u, 0u, 0u};
+    const double al = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
+        c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
+        in[4 * (size_t)a.n], a.mode, &work);
+    sp.alpha[(size_t)js * a.n + i] = al;
+    sp.awork[(size_t)js * a.n + i] =
+        (unsigned short)((work.n_active & 1u) | ((work.n_harm & 3u) << 1) | ((work.n_zero & 3u) << 3) |
+                         (min(work.n_terms, 2047u) << 5));
+}
+
+// RK4 ray_segment from x, N over `k` steps without stores (the NaN-alpha replay)
+__device__ void cold_replay(const TraceArgs &a, double x[3], double N[3], int k) {
+    SplitArgs none{};
+    for (int s = 0; s < k; s++) {
+        double xn[3], Nn[3];
+        cold_step<false>(a, none, 0, 0, x, N, xn, Nn);
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = xn[c];
+            N[c] = Nn[c];
+        }
+    }
+}
+
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    unsigned long long nsteps = 0, n_act = 0, n_harm = 0, n_terms = 0, n_zero = 0;
+    if (i < a.n) {
+        int steps = 0, st = ST_OK;
+        double tau = 0.0, psi_a = 0.0, Pdep = 0.0;
+        if (sp.k0 > 0) {
+            const int v = sp.sinfo[i];
+            steps = info_steps(v);
+            st = info_status(v);
+            tau = sp.stau[i];
+            Pdep = sp.sPdep[i];
+        }
+        if constexpr (DEPO == kDepoBinned) psi_a = sp.spsi[i];
+        if (st == ST_OK) {
+            const int tv = sp.tinfo[i];  // packed: steps and status written together
+            const int tT = info_steps(tv), tS = info_status(tv);
+            const double w = (DEPO == kDepoBinned && a.w) ? a.w[i] : 1.0;
+            const double ds6 = a.ds / 6.0;
+            double P = exp(-tau);  // bitwise the value the previous step computed
+            DepoAcc dacc = {-1, 0.0};
+            const int s_end = min(a.n_steps, sp.k0 + sp.kb);
+            for (int s = steps; s < s_end; s++) {
+                if (s >= tT) {  // the trajectory stopped before step s
+                    if (tS == ST_NAN) st = ST_NAN;  // non-finite x / N at step s (ray_segment's `bad`)
+                    break;
+                }
+                const size_t o = (size_t)(s - sp.k0) * 4 * a.n + i;
+                const double al0 = sp.alpha[o], al1 = sp.alpha[o + a.n], al2 = sp.alpha[o + 2 * (size_t)a.n],
+                             al3 = sp.alpha[o + 3 * (size_t)a.n];
+                double acc_a = fma(1.0, al0, 0.0);
+                acc_a = fma(2.0, al1, acc_a);
+                acc_a = fma(2.0, al2, acc_a);
+                acc_a = fma(1.0, al3, acc_a);
+                const double taun = tau + ds6 * acc_a;
+                if (!isfinite(taun)) {  // alpha went non-finite: NAN at step s, state x_s
+                    st = ST_NAN | 0x40;  // internal: the final state needs the replay
+                    break;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const unsigned wk = sp.awork[o + q * (size_t)a.n];
+                    n_act += wk & 1u;
+                    n_harm += (wk >> 1) & 3u;
+                    n_zero += (wk >> 3) & 3u;
+                    n_terms += wk >> 5;
+                }
+                const double Pn = exp(-taun);
+                const double dP = P - Pn;
+                if constexpr (DEPO == kDepoSamples) {
+                    if (s > 0) a.smp_dpds[smp_at(s, i, a.smp_rows)] = P * al0;
+                }
+                tau = taun;
+                P = Pn;
+                steps = s + 1;
+                nsteps++;
+                if constexpr (DEPO == kDepoBinned) {
+                    const double psi_b = sp.psib[(size_t)(s - sp.k0) * a.n + i];
+                    Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
+                    psi_a = psi_b;
+                }
+                if constexpr (TRAJ) {
+                    if (a.traj_stride > 0 && (steps % a.traj_stride) == 0)
+                        a.traj[((size_t)(steps / a.traj_stride - 1) * 5 + 3) * a.n + i] = tau;
+                }
+                if (steps == tT && tS == ST_LEFT_PLASMA) {  // psi check first (src/solve.jl:174)
+                    st = ST_LEFT_PLASMA;
+                    break;
+                }
+                if (a.chunk_steps > 0 && (steps % a.chunk_steps) == 0 && P < a.P_min) {  // :176
+                    st = ST_ABSORBED;
+                    break;
+                }
+            }
+            if constexpr (DEPO == kDepoBinned) depo_flush(a, dacc);
+            sp.stau[i] = tau;
+            sp.sPdep[i] = Pdep;
+            if constexpr (DEPO == kDepoBinned) sp.spsi[i] = psi_a;
+            sp.sinfo[i] = make_info(steps, st);
+        }
+    }
+    if (a.counters) {
+        const unsigned long long s0 = wave_sum(nsteps), s2 = wave_sum(n_act), s3 = wave_sum(n_harm),
+                                 s4 = wave_sum(n_terms), s5 = wave_sum(n_zero);
+        if (threadIdx.x == 0) {
+            atomicAdd(a.counters + 0, s0);
+            atomicAdd(a.counters + 1, 4ull * s0);
+            atomicAdd(a.counters + 2, s2);
+            atomicAdd(a.counters + 3, s3);
+            atomicAdd(a.counters + 4, s4);
+            atomicAdd(a.counters + 5, s5);
+        }
+    }
+}
+
+// final state, status and steps; trajectory samples past an earlier scan stop
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64) k_split_final(TraceArgs a, SplitArgs sp) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const int sv = sp.sinfo[i], tv = sp.tinfo[i];
+    const int steps = info_steps(sv), tT = info_steps(tv);
+    int st = info_status(sv);
+    double x[3], N[3];
+    if (steps == tT && !(st & 0x40)) {  // the scan ran to the trajectory's end: its carry
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = sp.tx[c * (size_t)a.n + i];
+            N[c] = sp.tx[(3 + c) * (size_t)a.n + i];
+        }
+    } else {  // stopped earlier: from the chunk-boundary state (+ replay to step `steps`)
+        const int cs = a.chunk_steps > 0 ? a.chunk_steps : 1 << 30;
+        const int c0 = a.chunk_steps > 0 ? steps / cs : 0;
+        const double *cb = sp.cbx + (size_t)c0 * 6 * a.n + i;
+#pragma unroll
+        for (int c = 0; c < 3; c++) {
+            x[c] = cb[c * (size_t)a.n];
+            N[c] = cb[(3 + c) * (size_t)a.n];
+        }
+        cold_replay(a, x, N, steps - c0 * (a.chunk_steps > 0 ? cs : 0));
+        if constexpr (TRAJ) {  // samples the trajectory wrote past the stop
+            if (a.traj_stride > 0)
+                for (int k = steps / a.traj_stride; k < min(tT, a.n_steps) / a.traj_stride; k++)
+                    for (int r = 0; r < 5; r++) a.traj[((size_t)k * 5 + r) * a.n + i] = NAN;
+        }
+    }
+    st &= 0x3f;
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+        a.state[c * a.n + i] = x[c];
+        a.state[(3 + c) * a.n + i] = N[c];
+    }
+    a.state[6 * a.n + i] = sp.stau[i];
+    a.status[i] = st;
+    a.steps[i] = steps;
+    const double Pdep = sp.sPdep[i];
+    if (a.Pdep) a.Pdep[i] = Pdep;
+    if constexpr (DEPO == kDepoBinned) {
+        const double w = a.w ? a.w[i] : 1.0;
+        atomicAdd(a.dP + a.n_psi, w * Pdep);  // sum_rays w P_dep
+    }
+}
+
+// ---------------------------------------------------------------------------
 // GPU ray entry (src/solve.jl:7-74): one lane per ray.  The bisection to the
 // psi_prof_max surface runs ~55 spline evaluations per lane; lanes of a wave
 // take nearly the same number, so 64-lane blocks keep divergence low.
@@ -1175,6 +1549,12 @@ struct torj_plasma_s {
     // single-process RCCL communicator over the first nccl_n of them
     std::vector<torj_plasma_s *> replicas;
     std::vector<ncclComm_t> comms;
+    // split RK4 path: workspace, the second stream of the
+    // alpha / scan kernels and the pipeline's events
+    void *d_split = nullptr;
+    size_t split_cap = 0;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_T[2] = {nullptr, nullptr}, ev_S[2] = {nullptr, nullptr}, ev_J = nullptr;
 };
 
 static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
@@ -1252,6 +1632,25 @@ static int ensure_fit(torj_plasma_s *p, size_t bytes) {
     p->fit_cap = 0;
     HIPCK(hipMalloc(&p->d_fit, bytes));
     p->fit_cap = bytes;
+    return 0;
+}
+
+static int ensure_split(torj_plasma_s *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (!p->stream2) {
+        HIPCK(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
+        for (int q = 0; q < 2; q++) {
+            HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
+            HIPCK(hipEventCreateWithFlags(&p->ev_S[q], hipEventDisableTiming));
+        }
+        HIPCK(hipEventCreateWithFlags(&p->ev_J, hipEventDisableTiming));
+    }
+    if (p->split_cap >= bytes) return 0;
+    if (p->d_split) HIPCK(hipFree(p->d_split));
+    p->d_split = nullptr;
+    p->split_cap = 0;
+    HIPCK(hipMalloc(&p->d_split, bytes));
+    p->split_cap = bytes;
     return 0;
 }
 
@@ -1478,6 +1877,13 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->d_chunk) (void)hipFree(p->d_chunk);
     for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
+    if (p->d_split) (void)hipFree(p->d_split);
+    for (int q = 0; q < 2; q++) {
+        if (p->ev_T[q]) (void)hipEventDestroy(p->ev_T[q]);
+        if (p->ev_S[q]) (void)hipEventDestroy(p->ev_S[q]);
+    }
+    if (p->ev_J) (void)hipEventDestroy(p->ev_J);
+    if (p->stream2) (void)hipStreamDestroy(p->stream2);
     delete p;
     return 0;
 }
@@ -1810,6 +2216,103 @@ int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N
     return 0;
 }
 
+}  // extern "C"
+
+// The split RK4 path's launches: per block of kb steps, the
+// trajectory kernel on `s`, the alpha and scan kernels on the handle's second
+// stream, double-buffered alpha inputs so the trajectory of block b + 1
+// overlaps the alpha of block b; joined back into `s`.
+static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, hipStream_t s) {
+    const size_t n = (size_t)a.n;
+    const int n_steps = a.n_steps;
+    // steps per block: two alpha-input buffers within the budget (TORJ_SPLIT_MB
+    // per buffer, default 4096), a multiple of the chunk length
+    static const size_t budget = [] {
+        const char *e = getenv("TORJ_SPLIT_MB");
+        return (size_t)(e ? atol(e) : 4096) << 20;
+    }();
+    const size_t per_step = 4 * kAinF * sizeof(double) * n;
+    long kb = (long)std::max<size_t>(1, budget / per_step);
+    if (a.chunk_steps > 0 && kb >= a.chunk_steps) kb -= kb % a.chunk_steps;
+    if (p->sched_mode == 3 && p->sched_waves > 0) kb = p->sched_waves;  // torj_set_sched(p, 3, steps per block)
+    kb = std::min<long>(kb, n_steps);
+    const int n_cb = (a.chunk_steps > 0 ? n_steps / a.chunk_steps : 0) + 1;
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t b_ain = al(per_step * kb), b_alpha = al(4 * sizeof(double) * n * kb),
+                 b_awork = al(4 * sizeof(unsigned short) * n * kb),
+                 b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
+                 b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
+    const int nq = (int)((n + 255) / 256);
+    const size_t bytes = 2 * b_ain + b_alpha + b_awork + 2 * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
+                         2 * b_n4;
+    if (ensure_split(p, bytes)) return -1;
+    char *q = (char *)p->d_split;
+    auto take = [&](size_t b) {
+        char *r = q;
+        q += b;
+        return r;
+    };
+    double *ain[2] = {(double *)take(b_ain), (double *)take(b_ain)};
+    SplitArgs sp{};
+    sp.alpha = (double *)take(b_alpha);
+    sp.awork = (unsigned short *)take(b_awork);
+    double *psib[2] = {nullptr, nullptr};
+    if (b_psib) psib[0] = (double *)take(b_psib), psib[1] = (double *)take(b_psib);
+    sp.cbx = (double *)take(b_cbx);
+    sp.tx = (double *)take(6 * b_n8);
+    sp.stau = (double *)take(b_n8);
+    sp.spsi = (double *)take(b_n8);
+    sp.sPdep = (double *)take(b_n8);
+    sp.tinfo = (int *)take(b_n4);
+    sp.sinfo = (int *)take(b_n4);
+
+    static const bool serial = [] {  // TORJ_SPLIT_SERIAL=1: no overlap (measurement aid)
+        const char *e = getenv("TORJ_SPLIT_SERIAL");
+        return e && atoi(e) != 0;
+    }();
+    hipStream_t s2 = serial ? s : p->stream2;
+    // the scan's carry starts at (steps 0, OK), tau = 0, P_dep = 0
+    HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, s));
+    HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, s));
+    const int G = (int)((n + 63) / 64);
+    const int n_blocks = (int)((n_steps + kb - 1) / kb);
+#define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
+    do {                                                                                    \
+        if (DM == kDepoSamples) {                                                           \
+            if (tr) hipLaunchKernelGGL((K<kDepoSamples, true>), __VA_ARGS__);               \
+            else hipLaunchKernelGGL((K<kDepoSamples, false>), __VA_ARGS__);                 \
+        } else if (DM == kDepoBinned) {                                                     \
+            if (tr) hipLaunchKernelGGL((K<kDepoBinned, true>), __VA_ARGS__);                \
+            else hipLaunchKernelGGL((K<kDepoBinned, false>), __VA_ARGS__);                  \
+        } else {                                                                            \
+            if (tr) hipLaunchKernelGGL((K<kDepoNone, true>), __VA_ARGS__);                  \
+            else hipLaunchKernelGGL((K<kDepoNone, false>), __VA_ARGS__);                    \
+        }                                                                                   \
+    } while (0)
+    for (int b = 0; b < n_blocks; b++) {
+        sp.k0 = (int)(b * kb);
+        sp.kb = (int)std::min<long>(kb, n_steps - sp.k0);
+        sp.ain = ain[b & 1];
+        sp.psib = psib[b & 1];
+        // this buffer's previous reader (alpha and scan of block b - 2) is done
+        if (b >= 2) HIPCK(hipStreamWaitEvent(s, p->ev_S[b & 1], 0));
+        TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, s, a, sp);
+        HIPCK(hipEventRecord(p->ev_T[b & 1], s));
+        HIPCK(hipStreamWaitEvent(s2, p->ev_T[b & 1], 0));
+        hipLaunchKernelGGL(k_alpha_pts, dim3((unsigned)(nq * 4 * sp.kb)), dim3(256), 0, s2, a, sp, nq);
+        TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s2, a, sp);
+        HIPCK(hipEventRecord(p->ev_S[b & 1], s2));
+    }
+    TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s2, a, sp);
+#undef TORJ_SPLIT_DISPATCH
+    HIPCK(hipEventRecord(p->ev_J, s2));
+    HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
+    HIPCK(hipGetLastError());
+    return 0;
+}
+
+extern "C" {
+
 int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                       const double *N0, const double *weights, int n_psi, const double *grid,
                       double *state, int *status, int *steps, double *dP, double *Pdep,
@@ -2001,7 +2504,18 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         p->ev_used += 3;
         HIPCK(hipEventRecord(ev[0], s));
     }
-    if (use_sched && cfg->n_steps > 0) {
+    static const int split_env = [] {
+        const char *e = getenv("TORJ_SPLIT");
+        return e ? atoi(e) : 1;
+    }();
+    // the split RK4 path: fixed steps, Albajar (sched mode 3, or by default for
+    // beams that would use the work queue)
+    const bool use_split = !adaptive && cfg->absorption == 1 && cfg->n_steps > 0 &&
+                           (p->sched_mode == 3 ||
+                            (p->sched_mode < 0 && split_env == 1 && sched_env && G > p->n_cu * 4));
+    if (use_split) {
+        if (split_trace(p, a, DM, tr, cs, s)) return -1;
+    } else if (use_sched && cfg->n_steps > 0) {
         // W persistent waves: at most 2 per SIMD (4 SIMDs per CU), and fewer
         // than G so the ready queue keeps a backlog (a wave never waits for a
         // group while another holds it); TORJ_SCHED_W overrides.
@@ -2120,7 +2634,7 @@ int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post
 
 int torj_set_sched(torj_plasma_t p, int mode, int waves) {
     if (!p) return fail("bad plasma handle");
-    if (mode < -1 || mode > 2) return fail("sched mode must be -1, 0, 1 or 2");
+    if (mode < -1 || mode > 3) return fail("sched mode must be -1, 0, 1, 2 or 3");
     if (waves < 0) return fail("waves must be >= 0");
     p->sched_mode = mode == 2 ? 0 : mode;
     p->lanes_per_ray = mode == 0 ? 1 : (mode == 2 ? 16 : 0);

@@ -624,7 +624,7 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
 }
 #endif
 
-template <int M, int LV, int LPR = 1>
+template <int M, int LV, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     SeriesCoefs<M, LV> sc;
     sc.load();
@@ -660,7 +660,6 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
         return s;
     }
 #endif
-    constexpr int U = TORJ_PAIR_UNROLL;
     double acc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = 0.0;
@@ -715,14 +714,15 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
 
 struct AlbajarWork {
     uint32_t n_active;  // calls that reached the harmonic loop
-    uint32_t n_harm;    // harmonic integrals evaluated
+    uint32_t n_harm;    // harmonic integrals evaluated (node loop run)
     uint32_t n_terms;   // Bessel-series terms evaluated (sum over node pairs of K)
+    uint32_t n_zero;    // harmonic integrals found exactly zero without the node loop
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
 // abs_Al_pol_fact) times sqrt((m/m_0)^2 - 1), WITHOUT the Maxwellian
 // normalisation a*(mu/2pi)^1.5 (common to both harmonics).
-template <int M, int LPR = 1>
+template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
                                 double inv_sqNp, double N_perp, double omega_bar,
                                 double Axz, double ea, double e3, AlbajarWork *work, int sub = 0) {
@@ -745,14 +745,34 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     c.C1 = c.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
     c.C2 = 2.0 * c.upa0 * c.upa1;
     c.hx = 0.5 * c.x_m;
+    // Exact zero: every node's exp(mu (1 - gamma)) underflows to +0 (exp_fast
+    // returns exactly 0 below -746) when mu (gamma_min - 1) exceeds 760, gamma_min
+    // the least gamma(t) = sqrt(C0 + C1 t^2 + C2 t) over t in [-1, 1] (a bound
+    // for every node of both signs, the vertex of the parabola or an end); the
+    // margin of 14 covers the rounding of gamma^2 and mu (1 - gamma).  Then every
+    // pair term is w p (P (0 + 0) + t Q (0 - 0)) = +-0 and the node sum is +-0:
+    // the loop is skipped with the same value (the sign of a zero aside, which
+    // no later operation sees) -- far from the resonance that is most of the
+    // third harmonic's evaluations on a beam.  NaN operands never skip.
+    const double qe = fma(c.C1, 1.0, c.C0) - fabs(c.C2);  // min of the ends t = -1, 1
+    const double tv = -c.C2 * 0.5 * rcp_nz(c.C1);          // vertex (C1 > 0)
+    const double qv = fma(-0.25 * c.C2, c.C2 * rcp_nz(c.C1), c.C0);
+    const double qmin = (c.C1 > 0.0 && fabs(tv) <= 1.0) ? qv : qe;
+    const bool zero = qmin > 1.0 && c.mu * (sqrt(qmin) - 1.0) > 760.0;
     // Bessel polynomial from the largest argument x_m (SeriesCoefs: x_m <= 1,
     // 2, 3, 4, each within a few ulp of mpmath's J_nu, checked in tests; the
     // 44-term Taylor loop beyond); physical rays have x_m < m.  The level is made
     // wave-uniform (max over the active lanes) so the node loop does not diverge.
     int level = c.x_m <= 1.0 ? 0 : (c.x_m <= 2.0 ? 1 : (c.x_m <= 3.0 ? 2 : (c.x_m <= kArgFast ? 3 : 4)));
+    if (zero) level = 0;  // a skipping lane does not raise the wave's polynomial length
 #ifdef __HIP_DEVICE_COMPILE__
     level = __ballot(level == 4) ? 4 : (__ballot(level == 3) ? 3 : (__ballot(level == 2) ? 2 : (__ballot(level == 1) ? 1 : 0)));
 #endif
+    const double Pm = md / (N_perp * omega_bar);
+    if (zero) {
+        if (work) work->n_zero++;
+        return -mu * Pm * Pm * 0.0 * sq_r;
+    }
     if (work) {
         constexpr int kTerms[5] = {series_terms(0), series_terms(1), series_terms(2), series_terms(3),
                                    kSeriesSlow};
@@ -760,15 +780,14 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     }
     double sum;
     switch (level) {
-        case 0: sum = node_sum<M, 0, LPR>(gl, c, sub); break;
-        case 1: sum = node_sum<M, 1, LPR>(gl, c, sub); break;
-        case 2: sum = node_sum<M, 2, LPR>(gl, c, sub); break;
-        case 3: sum = node_sum<M, 3, LPR>(gl, c, sub); break;
-        default: sum = node_sum<M, 4, LPR>(gl, c, sub); break;
+        case 0: sum = node_sum<M, 0, LPR, U>(gl, c, sub); break;
+        case 1: sum = node_sum<M, 1, LPR, U>(gl, c, sub); break;
+        case 2: sum = node_sum<M, 2, LPR, U>(gl, c, sub); break;
+        case 3: sum = node_sum<M, 3, LPR, U>(gl, c, sub); break;
+        default: sum = node_sum<M, 4, LPR, U>(gl, c, sub); break;
     }
     // (m / (N_perp omega_bar))^2: IEEE quotient, N_perp = 0 (parallel
     // propagation) stays an infinity as in the reference
-    const double Pm = md / (N_perp * omega_bar);
     return -mu * Pm * Pm * sum * sq_r;
 }
 
@@ -788,30 +807,41 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 #else
 #define TORJ_ALB_ATTR TORJ_HD
 #endif
-template <int LPR = 1>
-TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
-                                double N_par, double Te, int mode, AlbajarWork *work, int sub = 0) {
-    if (Te < 20.0) return 0.0;
+// The prologue of abs_Albajar_fast: everything the harmonic integrals and the
+// final normalisation need.  ok = false: alpha is 0 (the reference's early
+// returns, src/absorption.jl:191-212).
+struct AlbPro {
+    bool ok;
+    double inv_mu, mu, omega_bar, N_perp, inv_sqNp, Axz, ea, e3, m_0, inv_m0;
+};
+
+TORJ_HD AlbPro albajar_prologue(double X, double Y, double N_abs, double N_par, double Te,
+                                int mode) {
+    AlbPro q;
+    q.ok = false;
+    if (Te < 20.0) return q;
     constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te
-    const double inv_mu = Te * (1.0 / kMuTe);
-    const double mu = kMuTe * rcp_nz(Te);
+    q.inv_mu = Te * (1.0 / kMuTe);
+    q.mu = kMuTe * rcp_nz(Te);
     const double omega_bar = rcp_nz(Y);
+    q.omega_bar = omega_bar;
     const double cos_t = N_par * rcp_nz(N_abs);
     const double sin_t = sqrt(fma(-cos_t, cos_t, 1.0));
     const double N_perp = sqrt(N_abs * N_abs - N_par * N_par);
+    q.N_perp = N_perp;
     // abs_Al_N_with_pol_vec (src/absorption.jl:10-64), real form:
     // e = (e1, i*ea, e3) with e1, ea, e3 real.
-    if (X >= 1.0) return 0.0;
+    if (X >= 1.0) return q;
     const double s2 = sin_t * sin_t, c2 = cos_t * cos_t, omX = 1.0 - X;
     const double Y2 = Y * Y, invY2 = omega_bar * omega_bar;
     double rho = Y2 * (s2 * s2) + 4.0 * omX * omX * c2;
-    if (rho < 0.0) return 0.0;
+    if (rho < 0.0) return q;
     rho = sqrt(rho);
     const double f = (2.0 * omX) * rcp_nz(2.0 * omX - Y2 * s2 - (double)mode * Y * rho);
     double Nt = 1.0 - X * f;
-    if (Nt < 0.0) return 0.0;
+    if (Nt < 0.0) return q;
     Nt = sqrt(Nt);
-    if (!(Nt > 0.0) || Nt > 1.0) return 0.0;  // isnan || <= 0 || > 1
+    if (!(Nt > 0.0) || Nt > 1.0) return q;  // isnan || <= 0 || > 1
     const double inv_Nt = rcp_nz(Nt);
     const double g = 1.0 - (1.0 - Y2) * f;
     double e1 = 0.0, ea = 0.0, e3 = 0.0;
@@ -837,29 +867,57 @@ TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X,
     }
     const double omNp2 = 1.0 - N_par * N_par;
     const double sqNp = sqrt(omNp2);
-    const double m_0 = sqNp * omega_bar;
-    const double inv_sqNp = rcp_nz(sqNp);
-    const double N_eff = (N_perp * N_par) * (inv_sqNp * inv_sqNp);
-    const double Axz = e1 + N_eff * e3;
-    if (work) work->n_active++;
-    const double inv_m0 = inv_sqNp * Y;
-    double c_abs = 0.0;
-    if (!(2.0 < m_0)) {
-        c_abs += albajar_harmonic<2, LPR>(gl, mu, 2.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
-                                          Axz, ea, e3, work, sub);
-        if (work) work->n_harm++;
-    }
-    if (!(3.0 < m_0)) {  // src/absorption.jl:214 `if m < m_0 continue` (NaN m_0 -> NaN, as reference)
-        c_abs += albajar_harmonic<3, LPR>(gl, mu, 3.0 * inv_m0, N_par, inv_sqNp, N_perp, omega_bar,
-                                          Axz, ea, e3, work, sub);
-        if (work) work->n_harm++;
-    }
+    q.m_0 = sqNp * omega_bar;
+    q.inv_sqNp = rcp_nz(sqNp);
+    const double N_eff = (N_perp * N_par) * (q.inv_sqNp * q.inv_sqNp);
+    q.Axz = e1 + N_eff * e3;
+    q.ea = ea;
+    q.e3 = e3;
+    q.inv_m0 = q.inv_sqNp * Y;
+    q.ok = true;
+    return q;
+}
+
+// harmonic m of the sum (src/absorption.jl:213-223), if m >= m_0 (NaN m_0: no
+// harmonic, as the reference's `m < m_0` test makes it)
+template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
+TORJ_HD double albajar_pro_harmonic(const GLTable &gl, const AlbPro &q, double N_par,
+                                    AlbajarWork *work, int sub = 0) {
+    const uint32_t z0 = work ? work->n_zero : 0u;
+    const double h = albajar_harmonic<M, LPR, U>(gl, q.mu, (double)M * q.inv_m0, N_par, q.inv_sqNp,
+                                                 q.N_perp, q.omega_bar, q.Axz, q.ea, q.e3, work, sub);
+    if (work && work->n_zero == z0) work->n_harm++;
+    return h;
+}
+
+// the Maxwellian normalisation and units (src/absorption.jl:224-226)
+TORJ_HD double albajar_finish(const AlbPro &q, double c_abs, double X, double omega) {
     // 1 / (1 + 105/(128 mu^2) + 15/(8 mu)), (mu / 2 pi)^1.5
-    const double a = rcp_nz(fma(inv_mu, fma(inv_mu, 105.0 / 128.0, 15.0 / 8.0), 1.0));
-    const double sm = sqrt_pos(mu * (1.0 / (2.0 * kPi)));
+    const double a = rcp_nz(fma(q.inv_mu, fma(q.inv_mu, 105.0 / 128.0, 15.0 / 8.0), 1.0));
+    const double sm = sqrt_pos(q.mu * (1.0 / (2.0 * kPi)));
     c_abs *= a * (sm * sm * sm);
-    c_abs = -(c_abs * (2.0 * kPi * kPi) * inv_m0);
-    return c_abs * X * omega * (omega_bar * (1.0 / kC));
+    c_abs = -(c_abs * (2.0 * kPi * kPi) * q.inv_m0);
+    return c_abs * X * omega * (q.omega_bar * (1.0 / kC));
+}
+
+template <int LPR = 1, int U = TORJ_PAIR_UNROLL>
+TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, double Y,
+                                     double N_abs, double N_par, double Te, int mode,
+                                     AlbajarWork *work, int sub = 0) {
+    const AlbPro q = albajar_prologue(X, Y, N_abs, N_par, Te, mode);
+    if (!q.ok) return 0.0;
+    if (work) work->n_active++;
+    double c_abs = 0.0;
+    if (!(2.0 < q.m_0)) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, N_par, work, sub);
+    if (!(3.0 < q.m_0)) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, N_par, work, sub);
+    return albajar_finish(q, c_abs, X, omega);
+}
+// the fused trace kernels' call (out of line there, see TORJ_ALB_ATTR); kernels
+// with nothing else to hold (the split path's alpha kernel) inline the body
+template <int LPR = 1>
+TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
+                                double N_par, double Te, int mode, AlbajarWork *work, int sub = 0) {
+    return abs_albajar_fast_body<LPR>(gl, omega, X, Y, N_abs, N_par, Te, mode, work, sub);
 }
 
 // one RHS evaluation of sys! (src/solve.jl:112-114 -> gradΛ!, :85-95)
