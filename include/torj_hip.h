@@ -257,8 +257,8 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
  * steps pipelined over two streams (mode -1 picks it where it
  * would pick 1, unless env TORJ_SPLIT=0).
  * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16));
- * steps per pipeline block for mode 3 (0 = from the 4 GiB alpha-input budget,
- * env TORJ_SPLIT_MB). */
+ * steps per pipeline block for mode 3 (0 = from the 1 GiB per alpha-input
+ * buffer budget, env TORJ_SPLIT_MB; four buffers in flight). */
 int torj_set_sched(torj_plasma_t p, int mode, int waves);
 
 /* Waits for `stream` and checks every trace launched on this handle since

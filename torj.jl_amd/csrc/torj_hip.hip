@@ -1553,8 +1553,9 @@ struct torj_plasma_s {
     // alpha / scan kernels and the pipeline's events
     void *d_split = nullptr;
     size_t split_cap = 0;
-    hipStream_t stream2 = nullptr;
-    hipEvent_t ev_T[2] = {nullptr, nullptr}, ev_S[2] = {nullptr, nullptr}, ev_J = nullptr;
+    hipStream_t stream2 = nullptr, streamT = nullptr;  // alpha + scan; trajectory (high priority)
+    static constexpr int kRing = 4;                     // alpha-input buffers in flight
+    hipEvent_t ev_T[kRing] = {}, ev_S[kRing] = {}, ev_J = nullptr, ev_F = nullptr;
 };
 
 static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
@@ -1638,12 +1639,18 @@ static int ensure_fit(torj_plasma_s *p, size_t bytes) {
 static int ensure_split(torj_plasma_s *p, size_t bytes) {
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->stream2) {
-        HIPCK(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
-        for (int q = 0; q < 2; q++) {
+        // the trajectory chain is the critical path: its stream gets the highest
+        // priority, so its waves are dispatched ahead of the alpha kernel's
+        int lo = 0, hi = 0;
+        HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
+        HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
+        for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
             HIPCK(hipEventCreateWithFlags(&p->ev_S[q], hipEventDisableTiming));
         }
         HIPCK(hipEventCreateWithFlags(&p->ev_J, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&p->ev_F, hipEventDisableTiming));
     }
     if (p->split_cap >= bytes) return 0;
     if (p->d_split) HIPCK(hipFree(p->d_split));
@@ -1878,12 +1885,14 @@ int torj_plasma_destroy(torj_plasma_t p) {
     for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_split) (void)hipFree(p->d_split);
-    for (int q = 0; q < 2; q++) {
+    for (int q = 0; q < torj_plasma_s::kRing; q++) {
         if (p->ev_T[q]) (void)hipEventDestroy(p->ev_T[q]);
         if (p->ev_S[q]) (void)hipEventDestroy(p->ev_S[q]);
     }
     if (p->ev_J) (void)hipEventDestroy(p->ev_J);
+    if (p->ev_F) (void)hipEventDestroy(p->ev_F);
     if (p->stream2) (void)hipStreamDestroy(p->stream2);
+    if (p->streamT) (void)hipStreamDestroy(p->streamT);
     delete p;
     return 0;
 }
@@ -2219,18 +2228,21 @@ int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N
 }  // extern "C"
 
 // The split RK4 path's launches: per block of kb steps, the
-// trajectory kernel on `s`, the alpha and scan kernels on the handle's second
-// stream, double-buffered alpha inputs so the trajectory of block b + 1
-// overlaps the alpha of block b; joined back into `s`.
+// trajectory kernel on the handle's high-priority stream, the alpha and scan
+// kernels on its low-priority one, a ring of kRing alpha-input buffers so the
+// trajectory runs up to kRing blocks ahead of the alpha; forked from and
+// joined back into `s`.
 static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, hipStream_t s) {
     const size_t n = (size_t)a.n;
     const int n_steps = a.n_steps;
-    // steps per block: two alpha-input buffers within the budget (TORJ_SPLIT_MB
-    // per buffer, default 4096), a multiple of the chunk length
+    // steps per block: kRing alpha-input buffers within the budget (TORJ_SPLIT_MB
+    // per buffer, default 1024: measured 66.5 / 67.8 / 69.4 ms at 1 / 2 / 4 GiB on
+    // the headline beam), a multiple of the chunk length
     static const size_t budget = [] {
         const char *e = getenv("TORJ_SPLIT_MB");
-        return (size_t)(e ? atol(e) : 4096) << 20;
+        return (size_t)(e ? atol(e) : 1024) << 20;
     }();
+    constexpr int R = torj_plasma_s::kRing;
     const size_t per_step = 4 * kAinF * sizeof(double) * n;
     long kb = (long)std::max<size_t>(1, budget / per_step);
     if (a.chunk_steps > 0 && kb >= a.chunk_steps) kb -= kb % a.chunk_steps;
@@ -2243,7 +2255,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
     const int nq = (int)((n + 255) / 256);
-    const size_t bytes = 2 * b_ain + b_alpha + b_awork + 2 * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
+    const size_t bytes = R * b_ain + b_alpha + b_awork + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
                          2 * b_n4;
     if (ensure_split(p, bytes)) return -1;
     char *q = (char *)p->d_split;
@@ -2252,12 +2264,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         q += b;
         return r;
     };
-    double *ain[2] = {(double *)take(b_ain), (double *)take(b_ain)};
+    double *ain[R];
+    for (int r = 0; r < R; r++) ain[r] = (double *)take(b_ain);
     SplitArgs sp{};
     sp.alpha = (double *)take(b_alpha);
     sp.awork = (unsigned short *)take(b_awork);
-    double *psib[2] = {nullptr, nullptr};
-    if (b_psib) psib[0] = (double *)take(b_psib), psib[1] = (double *)take(b_psib);
+    double *psib[R] = {};
+    if (b_psib)
+        for (int r = 0; r < R; r++) psib[r] = (double *)take(b_psib);
     sp.cbx = (double *)take(b_cbx);
     sp.tx = (double *)take(6 * b_n8);
     sp.stau = (double *)take(b_n8);
@@ -2270,10 +2284,15 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const char *e = getenv("TORJ_SPLIT_SERIAL");
         return e && atoi(e) != 0;
     }();
-    hipStream_t s2 = serial ? s : p->stream2;
+    hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
+    if (!serial) {  // fork from the caller's stream
+        HIPCK(hipEventRecord(p->ev_F, s));
+        HIPCK(hipStreamWaitEvent(sT, p->ev_F, 0));
+        HIPCK(hipStreamWaitEvent(s2, p->ev_F, 0));
+    }
     // the scan's carry starts at (steps 0, OK), tau = 0, P_dep = 0
-    HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, s));
-    HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, s));
+    HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, sT));
+    HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, sT));
     const int G = (int)((n + 63) / 64);
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
@@ -2292,21 +2311,24 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     for (int b = 0; b < n_blocks; b++) {
         sp.k0 = (int)(b * kb);
         sp.kb = (int)std::min<long>(kb, n_steps - sp.k0);
-        sp.ain = ain[b & 1];
-        sp.psib = psib[b & 1];
-        // this buffer's previous reader (alpha and scan of block b - 2) is done
-        if (b >= 2) HIPCK(hipStreamWaitEvent(s, p->ev_S[b & 1], 0));
-        TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, s, a, sp);
-        HIPCK(hipEventRecord(p->ev_T[b & 1], s));
-        HIPCK(hipStreamWaitEvent(s2, p->ev_T[b & 1], 0));
+        const int r = b % R;
+        sp.ain = ain[r];
+        sp.psib = psib[r];
+        // this buffer's previous reader (alpha and scan of block b - R) is done
+        if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
+        TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
+        HIPCK(hipEventRecord(p->ev_T[r], sT));
+        HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
         hipLaunchKernelGGL(k_alpha_pts, dim3((unsigned)(nq * 4 * sp.kb)), dim3(256), 0, s2, a, sp, nq);
         TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s2, a, sp);
-        HIPCK(hipEventRecord(p->ev_S[b & 1], s2));
+        HIPCK(hipEventRecord(p->ev_S[r], s2));
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s2, a, sp);
 #undef TORJ_SPLIT_DISPATCH
-    HIPCK(hipEventRecord(p->ev_J, s2));
-    HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
+    if (!serial) {  // join: the final kernel followed every scan, and each scan its trajectory
+        HIPCK(hipEventRecord(p->ev_J, s2));
+        HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
+    }
     HIPCK(hipGetLastError());
     return 0;
 }
