@@ -115,3 +115,20 @@ def test_split_counters_match_fused(gpu, T, hplasma):
             hplasma.set_sched(-1)
         out.append((cnt.cpu().numpy(), state.cpu().numpy()))
     assert np.array_equal(out[0][0], out[1][0]), (out[0][0], out[1][0])
+
+
+def test_split_on_129_grid_vs_oracle(gpu, T, O):
+    """The split path on the 129 x 129 equilibrium, whose coefficients (1.1 MB)
+    do not fit LDS: the trajectory kernel reads them through L2."""
+    from test_gpu_parity import _compare_trace
+    from torj_hip import synthetic as S
+
+    eq = S.circular_tokamak(nR=129, nZ=129)
+    hp = T.Plasma(*S.plasma_args(eq))
+    op = O.OraclePlasma(*S.plasma_args(eq))
+    pos, xp, Np, s0, w, om = _fan(T, hp, n_rings=6)
+    grid = np.linspace(0, 1, 500)
+    g = _run(T, hp, 3, 0, xp, Np, om, 1, ds=1e-4, n_steps=2000, psi_grid=grid, weights=w)
+    o = op.trace(xp, Np, om, 1, 1e-4, 2000, psi_grid=grid, weights=w)
+    _compare_trace(g, o)
+    assert np.abs(g.dP_shell[:-1] - o["dP"]).max() <= 1e-10 * np.abs(o["dP"]).max()

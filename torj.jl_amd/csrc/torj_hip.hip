@@ -882,10 +882,10 @@ __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st
 
 // One cold RK4 step of ray_segment's arithmetic (plasma_point with ln Te, as
 // the absorbing kernels evaluate it); STORE: this step's alpha inputs -> ain.
-template <bool STORE>
-__device__ __forceinline__ bool cold_step(const TraceArgs &a, const SplitArgs &sp, int j, int i,
-                                          const double x[3], const double N[3], double xn[3],
-                                          double Nn[3]) {
+template <bool STORE, int NS = kNF>
+__device__ __forceinline__ bool cold_step(const TraceArgs &a, const double *__restrict__ coef,
+                                          const SplitArgs &sp, int j, int i, const double x[3],
+                                          const double N[3], double xn[3], double Nn[3]) {
     const double hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
     double acc[6] = {0, 0, 0, 0, 0, 0}, xt[3], Nt[3], k[6];
 #pragma unroll
@@ -896,7 +896,7 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, const SplitArgs &s
 #pragma unroll 1
     for (int st = 0; st < 4; st++) {
         PlasmaPoint p;
-        plasma_point<true>(a.coef, a.g, a.k, xt, p);
+        plasma_point<true, NS>(coef, a.g, a.k, xt, p);
         double Npar, inv;
         dispersion_grad(p, Nt, a.mode, k, &Npar, &inv);
         if constexpr (STORE) {
@@ -936,9 +936,22 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, const SplitArgs &s
 #ifndef TORJ_ALPHA_UNROLL  // node pairs per iteration of the alpha kernel's node loop (ILP)
 #define TORJ_ALPHA_UNROLL 1
 #endif
-template <int DEPO, bool TRAJ>
-__global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, SplitArgs sp) {
-    const int i = blockIdx.x * 64 + threadIdx.x;
+// LDS: the field coefficients staged in LDS (6 fp64 per node, 161 KB for a 56 x 56
+// grid; one workgroup of up to 8 waves per CU), measured against L2
+constexpr int kTrajLdsNS = 6;
+template <int DEPO, bool TRAJ, bool LDS>
+__device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &sp) {
+    constexpr int NS = LDS ? kTrajLdsNS : kNF;
+    const double *coef = a.coef;
+    if constexpr (LDS) {
+        extern __shared__ double s_coef[];
+        const int nodes = (a.g.nR + 2) * (a.g.nZ + 2);
+        for (int k = threadIdx.x; k < nodes * kTrajLdsNS; k += blockDim.x)
+            s_coef[k] = a.coef[(size_t)(k / kTrajLdsNS) * kNF + k % kTrajLdsNS];
+        __syncthreads();
+        coef = s_coef;
+    }
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= a.n) return;
     double x[3], N[3];
     int steps, st;
@@ -953,7 +966,7 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, Split
         steps = 0;
         st = ST_OK;
         if constexpr (DEPO != kDepoNone) {
-            const double psi0 = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+            const double psi0 = eval_one<NS>(coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
             sp.spsi[i] = psi0;  // the scan's psi_a at step 0
             if constexpr (DEPO == kDepoSamples) {
                 a.smp_psi[smp_at(0, i, a.smp_rows)] = psi0;
@@ -975,7 +988,7 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, Split
     const int s_end = min(a.n_steps, sp.k0 + sp.kb);
     for (int s = steps; s < s_end; s++) {
         double xn[3], Nn[3];
-        if (cold_step<true>(a, sp, s - sp.k0, i, x, N, xn, Nn)) {
+        if (cold_step<true, NS>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn)) {
             st = ST_NAN;
             break;
         }
@@ -988,7 +1001,7 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, Split
         const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
         double psi_b = 0.0;
         if (DEPO != kDepoNone || check)
-            psi_b = eval_one(a.coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+            psi_b = eval_one<NS>(coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
         if constexpr (DEPO == kDepoSamples) a.smp_psi[smp_at(steps, i, a.smp_rows)] = psi_b;
         if constexpr (DEPO == kDepoBinned) sp.psib[(size_t)(s - sp.k0) * a.n + i] = psi_b;
         if constexpr (TRAJ) {
@@ -1021,6 +1034,15 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, Split
     sp.tinfo[i] = make_info(steps, st);
 }
 
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, SplitArgs sp) {
+    traj_body<DEPO, TRAJ, false>(a, sp);
+}
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(512, 1) k_traj_lds(TraceArgs a, SplitArgs sp) {
+    traj_body<DEPO, TRAJ, true>(a, sp);
+}
+
 // alpha at the stored stage points of one block: block = 256 lanes = 4 groups
 // of 64 rays at one (step j, stage); lanes of rays the trajectory did not
 // reach this step with (or the scan has stopped) sit out, as in the fused wave
@@ -1050,7 +1072,7 @@ __device__ void cold_replay(const TraceArgs &a, double x[3], double N[3], int k)
     SplitArgs none{};
     for (int s = 0; s < k; s++) {
         double xn[3], Nn[3];
-        cold_step<false>(a, none, 0, 0, x, N, xn, Nn);
+        cold_step<false>(a, a.coef, none, 0, 0, x, N, xn, Nn);
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             x[c] = xn[c];
@@ -2294,6 +2316,17 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, sT));
     HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, sT));
     const int G = (int)((n + 63) / 64);
+    // the trajectory kernel with the coefficients staged in LDS whenever the grid
+    // fits 160 KiB at 6 fp64 per node (56 x 56: 161 KB), one workgroup of wpb
+    // waves per CU (measured: trajectory kernel 28.2 -> 24.3 ms, pipeline 67.2 ->
+    // 61.6 ms on the headline beam; TORJ_TRAJ_LDS=0 reads them through L2)
+    static const int lds_env = [] {
+        const char *e = getenv("TORJ_TRAJ_LDS");
+        return e ? atoi(e) : 1;
+    }();
+    const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
+    const bool lds_traj = lds_env == 1 && lds_bytes <= 160 * 1024;
+    const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
     do {                                                                                    \
@@ -2316,7 +2349,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.psib = psib[r];
         // this buffer's previous reader (alpha and scan of block b - R) is done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
-        TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
+        if (lds_traj)
+            TORJ_SPLIT_DISPATCH(k_traj_lds, dim3(nblocks(G, wpb)), dim3(64 * wpb), lds_bytes, sT, a, sp);
+        else
+            TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
         HIPCK(hipEventRecord(p->ev_T[r], sT));
         HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
         hipLaunchKernelGGL(k_alpha_pts, dim3((unsigned)(nq * 4 * sp.kb)), dim3(256), 0, s2, a, sp, nq);

@@ -173,7 +173,7 @@ struct FieldPack {
 // point is inside the grid on both axes (Line() extrapolation distances 0) and
 // skips the sums only the extrapolation needs (value-only fields' slopes, the
 // mixed derivative); the results are then identical to EXT = true.
-template <int NGRAD, int NVAL, bool EXT = true>
+template <int NGRAD, int NVAL, bool EXT = true, int NS = kNF>
 TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double R, double Z,
                          const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
     constexpr int NT = NGRAD + NVAL;
@@ -188,14 +188,14 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
     for (int f = 0; f < NT; f++) v[f] = gr[f] = gz[f] = grz[f] = 0.0;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
-        const double *row = coef + ((size_t)(aZ.i + b) * mR + aR.i) * kNF;
+        const double *row = coef + ((size_t)(aZ.i + b) * mR + aR.i) * NS;
 #pragma unroll
         for (int f = 0; f < NT; f++) {
             const bool slopes = EXT || f < NGRAD;
             double sv = 0.0, sd = 0.0;
 #pragma unroll
             for (int a = 0; a < 4; a++) {
-                const double c = row[a * kNF + fidx[f]];
+                const double c = row[a * NS + fidx[f]];
                 sv = fma(aR.w[a], c, sv);
                 if (slopes) sd = fma(aR.dw[a], c, sd);
             }
@@ -242,13 +242,14 @@ TORJ_HD bool inside_grid(const Grid &g, double R, double Z) {
 }
 
 // single value (e.g. psi for termination / deposition)
+template <int NS = kNF>
 TORJ_HD double eval_one(const double *__restrict__ coef, const Grid &g, double R, double Z, int field) {
     FieldPack<0, 1> p;
     const int idx[1] = {field};
     if (inside_grid(g, R, Z))
-        eval_fields<0, 1, false>(coef, g, R, Z, idx, p);
+        eval_fields<0, 1, false, NS>(coef, g, R, Z, idx, p);
     else
-        eval_fields<0, 1, true>(coef, g, R, Z, idx, p);
+        eval_fields<0, 1, true, NS>(coef, g, R, Z, idx, p);
     return p.v[0];
 }
 
@@ -329,7 +330,7 @@ TORJ_HD Consts make_consts(double omega) {
 }
 
 // fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te
-template <bool WITH_TE>
+template <bool WITH_TE, int NS = kNF>
 TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
     const double R = sqrt_pos(x[0] * x[0] + x[1] * x[1]);
@@ -341,16 +342,16 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     if constexpr (WITH_TE) {
         const int idx[5] = {F_BR, F_BPHI, F_BZ, F_LNNE, F_LNTE};
         if (in)
-            eval_fields<4, 1, false>(coef, g, R, x[2], idx, f);
+            eval_fields<4, 1, false, NS>(coef, g, R, x[2], idx, f);
         else
-            eval_fields<4, 1, true>(coef, g, R, x[2], idx, f);
+            eval_fields<4, 1, true, NS>(coef, g, R, x[2], idx, f);
         p.lnTe = f.v[4];
     } else {
         const int idx[4] = {F_BR, F_BPHI, F_BZ, F_LNNE};
         if (in)
-            eval_fields<4, 0, false>(coef, g, R, x[2], idx, f);
+            eval_fields<4, 0, false, NS>(coef, g, R, x[2], idx, f);
         else
-            eval_fields<4, 0, true>(coef, g, R, x[2], idx, f);
+            eval_fields<4, 0, true, NS>(coef, g, R, x[2], idx, f);
         p.lnTe = 0.0;
     }
     const double Br = f.v[0], Bp = f.v[1], Bz = f.v[2];
