@@ -1325,6 +1325,13 @@ static int ts_ray(const or_plasma *p, const or_trace_cfg *c, int r, double u[7],
                 const double Pa = u[6];
                 memcpy(u, ut, sizeof(double) * 7);
                 memcpy(k[0], k[6], sizeof(double) * 7);
+                /* ContinuousCallback(u[7] < 0, affect!) (src/solve.jl:78-83,159-160):
+                 * P projected to 0 at the end of the accepted step that crossed
+                 * (DiffEq root-finds the crossing inside the step: unpinned) */
+                if (u[6] < 0.0) {
+                    u[6] = 0.0;
+                    k[0][6] = -0.0;
+                }
                 t = tn;
                 steps++;
                 const double psi_b = or_evaluate(&p->psi, u);

@@ -99,3 +99,26 @@ def test_adaptive_capacity_status(gpu, T, hplasma, fan_states):
     g = T.trace(hplasma, xp[:3], Np[:3], om, 1, ds=1e-4, n_steps=150, integrator="adaptive",
                 s_max=0.2)
     assert np.all(g.status == T.MAX_STEPS) and np.all(g.steps == 150)
+
+
+def test_adaptive_power_clamp(gpu, T, hplasma, oplasma, fan_states):
+    """The reference's ContinuousCallback(u[7] < 0, affect!) (src/solve.jl:78-83,
+    159-160): with dtmax = 2 cm through the X2 layer, Tsit5's steps overshoot
+    P below zero (alpha ds >> 1); the power is projected back to 0, every saved
+    P is >= 0 and the ray stops ABSORBED at the next chunk boundary, as in the
+    oracle's identical restatement."""
+    xp, Np, w, om = fan_states[1]
+    idx = np.arange(0, len(w), 60)
+    kw = dict(ds=2e-2, n_steps=4000, traj_stride=1)
+    # loose tolerances: the steps are dtmax-limited (alpha ds ~ 10 in the layer)
+    g = T.trace(hplasma, xp[idx], Np[idx], om, 1, integrator="adaptive", s_max=0.4, n_chunks=20,
+                abstol=1.0, reltol=1.0, **kw)
+    o = oplasma.trace(xp[idx], Np[idx], om, 1, 2e-2, 4000, traj_stride=1, integrator=1, s_max=0.4,
+                      n_chunks=20, abstol=1.0, reltol=1.0)
+    P = np.exp(-g.traj[:, :, 3])
+    fin = np.isfinite(P)
+    assert fin.any() and (P[fin] >= 0.0).all()
+    assert (P[fin] == 0.0).any()  # the clamp engaged (the oracle: 15 saved P = 0)
+    assert (np.exp(-g.state[:, 6]) >= 0).all()
+    assert np.array_equal(g.status, o["status"])
+    assert T.ABSORBED in g.status.tolist()

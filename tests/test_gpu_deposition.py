@@ -157,3 +157,32 @@ def test_reference_deposition_grid_beyond_lds(gpu, T, hplasma, oplasma):
     # a fine grid makes near-grazing boundaries likelier (see the test above)
     assert np.abs(g.dP_shell[:-2] - shell).max() <= 1e-9 * scale
     assert np.abs(g.P_dep - P).max() <= 1e-9 * max(P.max(), 1e-300)
+
+
+def test_reference_deposition_in_ray_batches(gpu, T, hplasma):
+    """A beam whose reference-deposition workspace exceeds the budget
+    (TORJ_WS_GB) is traced in contiguous batches of whole 64-ray groups: every
+    per-ray output equals the single launch bit for bit, dP_shell to its
+    summation order."""
+    import os
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, 1, n_rings=14, min_az=5)
+    grid = np.linspace(0, 1, 1000)
+    kw = dict(ds=1e-4, n_steps=3000, psi_grid=grid, weights=w, deposition="reference", x_launch=pos,
+              s0=s0, traj_stride=100)
+    old = os.environ.get("TORJ_WS_GB")
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        os.environ["TORJ_WS_GB"] = "0.05"  # ~160 KB per ray: batches of 256 rays
+        b = T.trace(hplasma, xp, Np, om, 1, **kw)
+    finally:
+        hplasma.set_sched(-1)
+        if old is None:
+            os.environ.pop("TORJ_WS_GB", None)
+        else:
+            os.environ["TORJ_WS_GB"] = old
+    for f in ("state", "status", "steps", "P_dep"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()

@@ -306,21 +306,23 @@ def test_trace_golden_rays(gpu, T, hplasma):
 
 
 # ------------------------------------------------------------ API level
-def test_make_ray_matches_oracle(gpu, T, hplasma, oplasma):
-    """test_make_ray.jl shape: single X-mode ray, 85.5 GHz, s_max 0.4."""
+@pytest.mark.parametrize("mode", [1, -1])
+def test_make_ray_matches_oracle(gpu, T, hplasma, oplasma, mode):
+    """test_make_ray.jl shape / BASELINE configs[0] (C1): a single ray, 85.5 GHz,
+    s_max 0.4, X-mode (the reference file's +1) and O-mode (-1)."""
     from torj_hip import synthetic as S
 
     s = S.SETUP
     N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
     x0 = [s["R0"], 0.0, s["z0"]]
     grid = np.linspace(0, 1, 1000)
-    sv, u, P_beam, dP_dV, pdep = T.make_ray(hplasma, x0, N0, s["f"], 1, 0.4, grid,
+    sv, u, P_beam, dP_dV, pdep = T.make_ray(hplasma, x0, N0, s["f"], mode, 0.4, grid,
                                             deposition="binned")
     assert len(sv) == len(u) == len(P_beam) == 4002
     assert np.all(np.diff(sv) > 0) and sv[0] == 0.0
     om = 2 * np.pi * s["f"]
-    st, xp, Np, s0 = oplasma.ray_entry(x0, N0, om, 1)
-    o = oplasma.trace(xp[None], Np[None], om, 1, 1e-4, 4000, psi_grid=grid, traj_stride=1)
+    st, xp, Np, s0 = oplasma.ray_entry(x0, N0, om, mode)
+    o = oplasma.trace(xp[None], Np[None], om, mode, 1e-4, 4000, psi_grid=grid, traj_stride=1)
     assert np.abs(u[2:] - o["traj"][0, :, :3]).max() < 1e-9
     assert abs(pdep - o["Pdep"][0]) <= 1e-10 * max(o["Pdep"][0], 1e-300)
     dV = np.diff([oplasma.volume(p) for p in grid])

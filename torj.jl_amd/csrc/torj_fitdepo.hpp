@@ -220,11 +220,8 @@ TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, double
 //    monotone crossing of the boundary levels) form one run, flushed as a
 //    difference pair cdiff[lo] += 1, cdiff[hi + 1] -= 1, so cnt[k] is a prefix
 //    sum (one flush per turning point of psi(s), not one update per root);
-//  * a closed pair adds its |integral| to the shell (TORJ_DEPO_ATOMIC: no-return
-//    atomic; else a plain read-modify-write of the lane's own element).
-#ifndef TORJ_DEPO_ATOMIC
-#define TORJ_DEPO_ATOMIC 1
-#endif
+//  * a closed pair adds its |integral| to the shell with a no-return atomic on
+//    the lane's own element.
 constexpr int kOpenCache = 2;
 
 template <int NC = kOpenCache>
@@ -255,11 +252,7 @@ struct Walker {
     }
     TORJ_HD void close(int q, double d) {  // |integrate(dP_ds, r1, r2)|
         double *p = a->dPs + (size_t)q * a->n + i;
-#if TORJ_DEPO_ATOMIC
         __hip_atomic_fetch_add(p, d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-        *p += d;
-#endif
     }
     TORJ_HD void toggle(int q, double Fr) {
         bool hit = false;

@@ -586,6 +586,15 @@ __device__ void ray_chunk_tsit5(const TraceArgs &a, int i, double w, RayState &r
                 u[q] = ut[q];
                 K(0, q) = K(6, q);
             }
+            // the reference's ContinuousCallback(u[7] < 0, affect!): P is
+            // projected to 0 (src/solve.jl:78-83,159-160), applied at the end of
+            // the accepted step that crossed (DiffEq would root-find the crossing
+            // inside the step; that location is unpinned here), and the FSAL
+            // derivative follows: dP/ds = -P alpha = -0
+            if (u[6] < 0.0) {
+                u[6] = 0.0;
+                K(0, 6) = -0.0;
+            }
             t = tn;
             r.steps++;
             if constexpr (DEPO != kDepoNone) {
@@ -778,7 +787,8 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
                 }
                 store_state(a, i, r);
             } else {
-                if (r.status == ST_OK && ch < a.n_chunks) {
+                const bool ran = r.status == ST_OK && ch < a.n_chunks;
+                if (ran) {
                     const int s0 = r.steps;
                     if constexpr (DEPO == kDepoSamples) {
                         if (ch == 0) {  // entry point (src/solve.jl:151)
@@ -797,8 +807,10 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
                     }
                 }
                 a.chunk[i] = ch;
-                const double P = r.tau;
-                if (!alive) r.tau = -log(P);  // final state carries tau = -ln P
+                // the tau slot carries P while the ray runs and tau = -ln P once it
+                // has finished -- converted on the visit that finished it only (a
+                // finished ray of a live group is reloaded and stored again)
+                if (ran && !alive) r.tau = -log(r.tau);  // final state carries tau = -ln P
                 store_state(a, i, r);
             }
         }
@@ -1038,8 +1050,11 @@ template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, false>(a, sp);
 }
+#ifndef TORJ_TRAJ_LDS_WAVES
+#define TORJ_TRAJ_LDS_WAVES 1
+#endif
 template <int DEPO, bool TRAJ>
-__global__ void __launch_bounds__(512, 1) k_traj_lds(TraceArgs a, SplitArgs sp) {
+__global__ void __launch_bounds__(512, TORJ_TRAJ_LDS_WAVES) k_traj_lds(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, true>(a, sp);
 }
 
@@ -1556,6 +1571,9 @@ struct torj_plasma_s {
     void *d_fit = nullptr;                 // reference-faithful deposition workspace
     size_t fit_cap = 0;
     bool timing = false;                   // torj_timing: HIP events around each phase
+    int timing_calls = 0;                  // trace calls recorded since torj_timing(p, 1)
+    void *d_batch = nullptr;               // ray-batch staging of torj_trace_device_ex
+    size_t batch_cap = 0;
     std::vector<hipEvent_t> ev_pool;       // 3 per recorded call (start, trace end, post end)
     size_t ev_used = 0;
     double *d_ws = nullptr;        // per-ray workspace (P_dep when the caller passes none)
@@ -1907,6 +1925,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     for (hipEvent_t e : p->ev_pool) (void)hipEventDestroy(e);
     if (p->d_ws) (void)hipFree(p->d_ws);
     if (p->d_split) (void)hipFree(p->d_split);
+    if (p->d_batch) (void)hipFree(p->d_batch);
     for (int q = 0; q < torj_plasma_s::kRing; q++) {
         if (p->ev_T[q]) (void)hipEventDestroy(p->ev_T[q]);
         if (p->ev_S[q]) (void)hipEventDestroy(p->ev_S[q]);
@@ -2379,12 +2398,107 @@ int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const d
                                 status, steps, dP, Pdep, traj, counters, stream);
 }
 
+}  // extern "C"
+
+static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                            const double *N0, const double *weights, int n_psi, const double *grid,
+                            const double *x_launch, const double *s0, double *state, int *status,
+                            int *steps, double *dP, double *Pdep, double *traj, uint64_t *counters,
+                            void *stream);
+
+// Device-memory budget of one launch's per-ray workspace (the reference
+// deposition's per-step samples and elimination coefficients, root counts and
+// shell arrays: ~116 KB per ray at 2 000 steps and 1 000 shells).  A beam whose
+// workspace would exceed it is traced in contiguous batches of whole 64-ray
+// groups, each batch's inputs gathered into and outputs scattered from
+// compact device buffers (TORJ_WS_GB, default 16).
+static size_t ws_budget() {
+    const char *e = getenv("TORJ_WS_GB");  // read per call (tests vary it)
+    const double g = e ? atof(e) : 16.0;
+    return (size_t)(g * (double)(1ull << 30));
+}
+
+static int ensure_batch(torj_plasma_s *p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (p->batch_cap >= bytes) return 0;
+    if (p->d_batch) HIPCK(hipFree(p->d_batch));
+    p->d_batch = nullptr;
+    p->batch_cap = 0;
+    HIPCK(hipMalloc(&p->d_batch, bytes));
+    p->batch_cap = bytes;
+    return 0;
+}
+
+extern "C" {
+
 int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                          const double *N0, const double *weights, int n_psi, const double *grid,
                          const double *x_launch, const double *s0, double *state, int *status,
                          int *steps, double *dP, double *Pdep, double *traj, uint64_t *counters,
                          void *stream) {
     if (!p || !cfg) return fail("bad plasma handle or cfg");
+    if (n <= 0) return 0;
+    if (p->timing) p->timing_calls++;
+    const bool fit = n_psi >= 2 && grid && dP && cfg->deposition == 1;
+    if (fit && cfg->n_steps > 0 && x0 && N0 && state && status && steps) {
+        const size_t K = (size_t)cfg->n_steps + 2, L = (size_t)n_psi;
+        const size_t per_ray = (cfg->integrator == 1 ? 6 : 5) * 8 * K + 4 * (L + 1) + 16 * L + 4;
+        if ((size_t)n * per_ray > ws_budget()) {
+            const int nb = (int)std::max<size_t>(64, ws_budget() / per_ray / 64 * 64);
+            if (ensure_device(p)) return -1;
+            hipStream_t s = (hipStream_t)stream;
+            const int n_save = cfg->traj_stride > 0 && traj ? cfg->n_steps / cfg->traj_stride : 0;
+            const size_t D = sizeof(double), B = (size_t)nb;
+            // staging: x0, N0, x_launch (3 rows), w, s0, P_dep (1), state (7), traj (5 n_save);
+            // status, steps (int)
+            const size_t rows = 3 + 3 + 3 + 1 + 1 + 1 + 7 + 5 * (size_t)n_save;
+            if (ensure_batch(p, rows * B * D + 2 * B * sizeof(int))) return -1;
+            double *q = (double *)p->d_batch;
+            double *bx0 = q, *bN0 = bx0 + 3 * B, *bxl = bN0 + 3 * B, *bw = bxl + 3 * B, *bs0 = bw + B,
+                   *bP = bs0 + B, *bst = bP + B, *btr = bst + 7 * B;
+            int *bstat = (int *)(btr + 5 * (size_t)n_save * B), *bsteps = bstat + B;
+            for (int lo = 0; lo < n; lo += nb) {
+                const int c = std::min(nb, n - lo);
+                auto gather = [&](double *d, const double *h, int r) -> int {
+                    if (!h) return 0;
+                    HIPCK(hipMemcpy2DAsync(d, c * D, h + lo, (size_t)n * D, c * D, r,
+                                           hipMemcpyDeviceToDevice, s));
+                    return 0;
+                };
+                auto scatter = [&](double *h, const double *d, int r) -> int {
+                    if (!h) return 0;
+                    HIPCK(hipMemcpy2DAsync(h + lo, (size_t)n * D, d, c * D, c * D, r,
+                                           hipMemcpyDeviceToDevice, s));
+                    return 0;
+                };
+                if (gather(bx0, x0, 3) || gather(bN0, N0, 3) || gather(bxl, x_launch, 3) ||
+                    gather(bw, weights, 1) || gather(bs0, s0, 1))
+                    return -1;
+                if (trace_device_one(p, cfg, c, bx0, bN0, weights ? bw : nullptr, n_psi, grid,
+                                     x_launch ? bxl : nullptr, s0 ? bs0 : nullptr, bst, bstat, bsteps,
+                                     dP, bP, n_save ? btr : nullptr, counters, stream))
+                    return -1;
+                if (scatter(state, bst, 7) || scatter(Pdep, bP, 1) ||
+                    scatter(n_save ? traj : nullptr, btr, 5 * n_save))
+                    return -1;
+                HIPCK(hipMemcpyAsync(status + lo, bstat, c * sizeof(int), hipMemcpyDeviceToDevice, s));
+                HIPCK(hipMemcpyAsync(steps + lo, bsteps, c * sizeof(int), hipMemcpyDeviceToDevice, s));
+            }
+            return 0;
+        }
+    }
+    return trace_device_one(p, cfg, n, x0, N0, weights, n_psi, grid, x_launch, s0, state, status,
+                            steps, dP, Pdep, traj, counters, stream);
+}
+
+}  // extern "C"
+
+// one launch of the hot path over n rays (the body of torj_trace_device_ex)
+static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
+                            const double *N0, const double *weights, int n_psi, const double *grid,
+                            const double *x_launch, const double *s0, double *state, int *status,
+                            int *steps, double *dP, double *Pdep, double *traj, uint64_t *counters,
+                            void *stream) {
     if (n <= 0) return 0;
     if (!x0 || !N0 || !state || !status || !steps) return fail("x0, N0, state, status, steps required");
     if (cfg->n_steps < 0) return fail("n_steps < 0");
@@ -2449,14 +2563,16 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
         // per-boundary root counts, per-shell open-root integrals
         const size_t K = (size_t)cfg->n_steps + 2, N = (size_t)n, L = (size_t)n_psi;
         const size_t KN = smp_elems(N, K);  // smp_at layout: 64-ray blocks of K rows
-        const size_t b_smp = 3 * KN * sizeof(double), b_m = 3 * KN * sizeof(double);
+        // arc lengths are stored by the adaptive integrator only (RK4: s0 + k ds)
+        const size_t n_smp = cfg->integrator == 1 ? 3 : 2;
+        const size_t b_smp = n_smp * KN * sizeof(double), b_m = 3 * KN * sizeof(double);
         const size_t b_cnt = ((L + 1) * N * sizeof(int) + 255) & ~(size_t)255, b_fo = L * N * sizeof(double);
         const size_t b_ks = (N * sizeof(int) + 255) & ~(size_t)255;
         if (ensure_fit(p, b_smp + b_m + b_cnt + 2 * b_fo + b_ks)) return -1;
         char *base = (char *)p->d_fit;
         a.smp_psi = (double *)base;
         a.smp_dpds = a.smp_psi + KN;
-        a.smp_s = a.smp_dpds + KN;
+        a.smp_s = cfg->integrator == 1 ? a.smp_dpds + KN : nullptr;
         a.smp_rows = K;
         fa.rows = K;
         fa.E = (double *)(base + b_smp);
@@ -2665,10 +2781,13 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     return 0;
 }
 
+extern "C" {
+
 int torj_timing(torj_plasma_t p, int enable) {
     if (!p) return fail("bad plasma handle");
     p->timing = enable != 0;
     p->ev_used = 0;
+    p->timing_calls = 0;
     return 0;
 }
 
@@ -2683,10 +2802,11 @@ int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post
         t += a;
         q += b;
     }
-    if (calls) *calls = (int)(p->ev_used / 3);
+    if (calls) *calls = p->timing_calls;  // a batched call records one triple per batch
     if (trace_ms) *trace_ms = t;
     if (post_ms) *post_ms = q;
     p->ev_used = 0;
+    p->timing_calls = 0;
     return 0;
 }
 

@@ -68,11 +68,7 @@ TORJ_HD double clampd(double x, double lo, double hi) { return x > hi ? hi : (x 
 // finite; the callers only pass denominators that are finite and non-zero on
 // every physical input (a zero means a resonance/cutoff the reference also
 // turns into a non-finite result).
-#ifndef TORJ_FAST_RCP
-#define TORJ_FAST_RCP 1
-#endif
 TORJ_HD double rcp_nz(double x) {
-#if TORJ_FAST_RCP
 #ifdef __HIP_DEVICE_COMPILE__
     double r = __builtin_amdgcn_rcp(x);
 #else
@@ -82,20 +78,14 @@ TORJ_HD double rcp_nz(double x) {
     r = fma(r, e, r);
     e = fma(-x, r, 1.0);
     return fma(r, e, r);
-#else
-    return 1.0 / x;
-#endif
 }
 
 // sqrt of a finite positive normal argument (lengths, |B|, |dD/dN|, the
 // node-loop gamma): on the device v_rsq_f64 + one Goldschmidt step + one Newton
 // correction (~1 ulp; the library sequence adds a second correction for correct
 // rounding plus denormal scaling and class checks).
-#ifndef TORJ_FAST_NODE_MATH
-#define TORJ_FAST_NODE_MATH 1
-#endif
 TORJ_HD double sqrt_pos(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+#if defined(__HIP_DEVICE_COMPILE__)
     const double y = __builtin_amdgcn_rsq(x);
     double g = x * y, h = 0.5 * y;
     const double r = fma(-h, g, 0.5);
@@ -112,7 +102,7 @@ TORJ_HD double sqrt_pos(double x) {
 // and underflows to 0 below ~-745, NaN stays NaN.  Used for the node loop's
 // exp(mu (1 - gamma)) and for n_e, T_e from their log splines.
 TORJ_HD double exp_fast(double x) {
-#if defined(__HIP_DEVICE_COMPILE__) && TORJ_FAST_NODE_MATH
+#if defined(__HIP_DEVICE_COMPILE__)
     const double k = __builtin_rint(x * 1.4426950408889634074);
     double r = fma(-k, 6.93147180559945286227e-01, x);
     r = fma(-k, 2.31904681384629955842e-17, r);
@@ -493,7 +483,7 @@ TORJ_HD void series_pair_loop(double z, double &Sa, double &Sb) {
 // Per-harmonic constants of the node sum (abs_Al_pol_fact / abs_Al_integral_nume_fast)
 struct HarmConst {
     double x_m, K0, K1, K2, K3, K4, K5, upa0, upa1, r2m1, mu;
-    // node-pair form (TORJ_PAIR_V2): gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
+    // node-pair form: gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
     double C0, C1, C2, hx;
 };
 
@@ -511,18 +501,10 @@ struct HarmConst {
 // Series coefficients of one harmonic for the node loop (compile-time
 // constants: the Horner FMAs take them as SGPR operands).
 // LV 0..3: the near-minimax polynomials of torj_bessel_coefs.hpp on x_m <= 1, 2,
-// 3, 4 (7 / 9 / 10 / 11 terms; TORJ_BESSEL_ECON=0: the Taylor series, 9 / 12 / 14
-// / 16 terms, same accuracy); LV 4: the 44-term Taylor loop (x_m <= 12).
-#ifndef TORJ_BESSEL_ECON
-#define TORJ_BESSEL_ECON 1
-#endif
-constexpr int kTaylorTerms[4] = {9, 12, 14, kSeriesFast};
-constexpr int series_terms(int lv) {
-    return lv >= 4 ? 0 : (TORJ_BESSEL_ECON ? kBesselTerms[lv] : kTaylorTerms[lv]);
-}
-constexpr double level_coef(int lv, int nu, int k) {
-    return TORJ_BESSEL_ECON ? kBesselCoef[lv][nu - 2][k] : series_coef(nu, k);
-}
+// 3, 4 (7 / 9 / 10 / 11 terms, as accurate as the 9 / 12 / 14 / 16-term Taylor
+// series they replaced); LV 4: the 44-term Taylor loop (x_m <= 12).
+constexpr int series_terms(int lv) { return lv >= 4 ? 0 : kBesselTerms[lv]; }
+constexpr double level_coef(int lv, int nu, int k) { return kBesselCoef[lv][nu - 2][k]; }
 
 template <int M, int LV>
 struct SeriesCoefs {
@@ -554,10 +536,6 @@ struct SeriesCoefs {
 };
 
 
-#ifndef TORJ_PAIR_V2
-#define TORJ_PAIR_V2 1
-#endif
-#if TORJ_PAIR_V2
 // The two nodes of a pair share every t-even factor.  With
 //   bracket(+-t) = P +- t Q,  P = A (K0 + K3 t^2) - B + Cc K1,  Q = A K4 + Cc K5
 //   gamma(+-t)^2 = (u_par0 +- u_par1 t)^2 + 1 + (r^2-1)(1-t^2) = C0 + C1 t^2 +- C2 t
@@ -591,39 +569,6 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double Em = exp_fast(fma(-c.mu, sqrt_pos(a - b), c.mu));
     return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
-#else
-template <int M, int LV>
-TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double st,
-                         double w, double, bool single) {
-    constexpr double md = (double)M;
-    const double arg = c.x_m * st;
-    const double h = 0.5 * arg;
-    const double h2 = h * h;
-    double Sm, Sm1;
-    sc.eval(-h2, Sm, Sm1);
-    const double Sl = md * Sm - h2 * Sm1;
-    double p = h;  // h^(2m-1)
-#pragma unroll
-    for (int k = 1; k < 2 * M - 1; k++) p *= h;
-    const double A = h * (Sm * Sm);
-    const double B = h * (c.K2 * h2 * Sl * Sm1);
-    const double Cc = st * Sm * (Sl - h2 * Sm1);
-    const double wp = w * p;
-    const double u_perp1 = 1.0 + c.r2m1 * (1.0 - t * t);
-    // +t
-    const double brp = A * fma(t, fma(c.K3, t, c.K4), c.K0) - B + Cc * fma(c.K5, t, c.K1);
-    const double upp = fma(c.upa1, t, c.upa0);
-    const double gp = sqrt_pos(fma(upp, upp, u_perp1));
-    double r = (wp * brp) * exp_fast(c.mu * (1.0 - gp));
-    if (!single) {  // -t
-        const double brm = A * fma(-t, fma(-c.K3, t, c.K4), c.K0) - B + Cc * fma(-c.K5, t, c.K1);
-        const double upm = fma(-c.upa1, t, c.upa0);
-        const double gm = sqrt_pos(fma(upm, upm, u_perp1));
-        r += (wp * brm) * exp_fast(c.mu * (1.0 - gm));
-    }
-    return r;
-}
-#endif
 
 template <int M, int LV, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {

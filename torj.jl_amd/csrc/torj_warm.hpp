@@ -385,17 +385,10 @@ TORJ_HD cplx faddeeva_upper(double x, double y) {
     return w;
 }
 
-#ifndef TORJ_FADDEEVA_WEIDEMAN
-#define TORJ_FADDEEVA_WEIDEMAN 1
-#endif
 // Z(z) = i sqrt(pi) w(z) (zetac, :345-465); the warm tensor's arguments all
 // have Im z >= 0 (zetac_upper); TOMS 680 serves Im z < 0
 TORJ_HD cplx zetac_upper(double x, double y) {
-#if TORJ_FADDEEVA_WEIDEMAN
     const cplx w = faddeeva_upper(x, y);
-#else
-    const cplx w = faddeeva(x, y);
-#endif
     return {-kSqrtPi * w.im, kSqrtPi * w.re};
 }
 TORJ_HD cplx zetac(double x, double y) {
