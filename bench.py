@@ -68,6 +68,8 @@ def parse():
                          "ranges) instead of one rotated fan per rank; e.g. --n-rings 291 --shard "
                          "for the ~1e6-ray beam over 8 GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-api", action="store_true",
+                    help="skip the host-pointer (PCIe-inclusive) call (profiling passes)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
     return ap.parse_args()
@@ -133,7 +135,7 @@ def main():
     cap = 2 * args.n_steps + 400 if adaptive else args.n_steps  # accepted-step capacity
     n_save = (cap if adaptive else args.n_steps) // args.traj_stride if args.traj_stride > 0 else 0
     d_traj = torch.empty((max(n_save, 1), 5, n), dtype=torch.float64, device=dev)
-    d_cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+    d_cnt = torch.zeros(8, dtype=torch.int64, device=dev)
     dep = 1 if args.deposition == "reference" else 0
     cfg = T._lib.TraceCfg(omega, args.mode, args.ds, cap, max(1, args.n_steps // 100),
                           1.0, 1e-6, ABSORPTION[args.absorption], args.traj_stride, dep,
@@ -214,11 +216,12 @@ def main():
 
     if rank == 0:
         status = d_status.cpu().numpy()
-        flop = F.algorithmic_flops(cnt, n_gl=24) if args.absorption in ("albajar", "none") else None
+        flop = (F.algorithmic_flops(cnt, n_gl=24) if args.absorption in ("albajar", "none")
+                else F.algorithmic_flops_warm(cnt) if args.absorption == "warm_wr" else None)
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         sched = adaptive or (os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd)
         dm = 2 if args.deposition == "reference" else 1
-        at = min(ABSORPTION[args.absorption], 2)  # ABS template: 0 cold, 1 Albajar, 2 warm
+        at = ABSORPTION[args.absorption]  # ABS template: 0 cold, 1 Albajar, 2 / 3 warm iwarm 1 / 3
         # the library's default for a large fixed-step Albajar beam: the split
         # pipeline -- its kernels are timed together as the trace phase
         split = (sched and not adaptive and args.absorption == "albajar"
@@ -232,10 +235,14 @@ def main():
                  else f"k_trace<{at}, {dm}, true>")  # rocprof's name of the instance
         traffic = measured_traffic(kname, n, args)
         kern_s = float(km[0].item()) / 1e3
-        flop_source = "algorithmic (torj_hip/flops.py x the kernel's work counters)"
+        flop_source = ("algorithmic (torj_hip/flops.py algorithmic_flops_warm x the kernel's "
+                       "8 work counters; a lower bound, oracle/flopcount_warm.py)"
+                       if args.absorption == "warm_wr"
+                       else "algorithmic (torj_hip/flops.py x the kernel's work counters)")
         if flop is None and traffic and traffic.get("fp64_flops_executed"):
-            # warm alpha: no op-count model; executed fp64 VALU FLOPs of the same
-            # kernel and workload from the committed PMC profile
+            # warm_fr: no op-count model (its t-quadrature's expei branches);
+            # executed fp64 VALU FLOPs of the same kernel and workload from the
+            # committed PMC profile
             flop = traffic["fp64_flops_executed"]
             flop_source = f"executed: PMC SQ_INSTS_VALU_*_F64 x 64 lanes ({traffic['file']})"
         achieved = flop / kern_s / 1e12 if flop is not None else None
@@ -298,12 +305,18 @@ def main():
                 "flop_source": flop_source if flop is not None else None,
                 "flop_per_ray_step": flop / max(cnt[0], 1) if flop is not None else None,
             },
-            "work_counters": {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
-                              "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
-                              "bessel_series_terms": int(cnt[4]),
-                              "harmonic_integrals_exact_zero": int(cnt[5])},
+            "work_counters": (
+                {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
+                 "larmor_tests": int(cnt[2]), "faddeeva_evals": int(cnt[3]),
+                 "warmdisp_passes": int(cnt[4]), "passes_x_lrm": int(cnt[5]),
+                 "sum_lrm": int(cnt[6]), "sum_lrm2": int(cnt[7])}
+                if args.absorption == "warm_wr" else
+                {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
+                 "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
+                 "bessel_series_terms": int(cnt[4]),
+                 "harmonic_integrals_exact_zero": int(cnt[5])}),
         }
-        if world == 1:
+        if world == 1 and not args.no_host_api:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,
                                             pos, s0)
             progress("host-pointer call done")
@@ -411,12 +424,12 @@ def pipeline_kernel_ms(stats_csv, kernels):
 
 
 def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
-    """The CPU oracle (C restatement, OpenMP) on a bounded sample of the same rays.
-    Warm models: the C oracle's RK4 with oracle/warm_ref.py's numpy alpha through
-    a callback (serial), on a shorter sample (rays x steps sized to ~cpu_seconds).
+    """The CPU oracle (C restatement, OpenMP on every host core) on a bounded
+    sample of the same rays, warm models included (oracle/torj_warm_oracle.c).
     Returns (cpu_baseline, parity): when the sample runs the full n_steps, parity
     compares its endpoints with the timed launches' GPU outputs for the same rays
-    (status / steps exact, max relative error of x, N, tau; bar 1e-10)."""
+    (status / steps exact, max relative error of x, N, tau; bar 1e-10, warm models
+    the tests' 1e-8 / 1e-9 on tau, tests/test_gpu_warm.py)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from torj_hip import synthetic as S
@@ -425,24 +438,16 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
     O.abs_al_init(24)
     model = ABSORPTION[args.absorption]
     warm = model >= 2
-    threads = 1 if warm else O.default_threads()
+    threads = O.default_threads()
     kw = dict(psi_grid=grid, absorption=model, n_threads=threads)
-    # calibration sample (warm: one ray over its first 50 steps, after a
-    # 2-step call that pays the callback's first-use cost)
-    cal_steps = min(args.n_steps, 50) if warm else args.n_steps
+    # calibration sample: one ray per thread over the full path
     idx = np.linspace(0, len(w) - 1, num=threads, dtype=int)
-    if warm:
-        OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, 2, weights=w[idx], **kw)
     t0 = time.perf_counter()
-    OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, cal_steps, weights=w[idx], **kw)
+    OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, weights=w[idx], **kw)
     t_cal = time.perf_counter() - t0
     scale = max(1.0, args.cpu_seconds / max(t_cal, 1e-3))
-    if warm:
-        n_steps = int(min(args.n_steps, cal_steps * scale))
-        n_rays = int(max(1, min(len(w), cal_steps * scale / max(n_steps, 1))))
-    else:
-        n_steps = args.n_steps
-        n_rays = int(max(threads, min(len(w), threads * round(scale))))
+    n_steps = args.n_steps
+    n_rays = int(max(threads, min(len(w), threads * round(scale))))
     idx = np.linspace(0, len(w) - 1, num=n_rays, dtype=int)
     t0 = time.perf_counter()
     r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, n_steps, weights=w[idx], **kw)
@@ -464,8 +469,9 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
                   "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
                   "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
                   "max_rel_tau_unfloored": float(et_strict.max()),
-                  "max_rel": float(max(ex.max(), eN.max(), et.max())), "bar": 1e-10}
-    what = ("oracle/torj_oracle.c RK4 + oracle/warm_ref.py numpy alpha (callback, serial)" if warm
+                  "max_rel": float(max(ex.max(), eN.max(), et.max())),
+                  "bar": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)}
+    what = ("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
             else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_rays} rays (evenly spaced over the same fan) x {n_steps} RK4 steps, "

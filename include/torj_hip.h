@@ -34,7 +34,7 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 3  /* 3: torj_trace_beam, sticky launch flags */
+#define TORJ_ABI_VERSION 4  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -207,10 +207,16 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
 
 /* Device-pointer form (inputs resident in HBM; what bench.py times).
  * dP_shell (n_psi+1) is ACCUMULATED into (zero it first).  counters (may be
- * NULL): 6 x uint64 accumulated: ray-steps, RHS evaluations, absorption calls
- * reaching the harmonic sum, harmonic integrals evaluated, Bessel-series terms,
- * harmonic integrals found exactly zero without their node loop -- the basis
- * of the algorithmic FLOP count.  stream: hipStream_t or NULL. */
+ * NULL): 8 x uint64 accumulated, the basis of the algorithmic FLOP count
+ * (torj_hip/flops.py): [0] ray-steps, [1] RHS evaluations, then
+ *   absorption 1 (Albajar): [2] calls reaching the harmonic sum, [3] harmonic
+ *     integrals evaluated, [4] Bessel-series terms, [5] harmonic integrals found
+ *     exactly zero without their node loop, [6] [7] 0;
+ *   absorption 2 (warm, iwarm 1): [2] larmornumber tests, [3] Faddeeva
+ *     evaluations, [4] warmdisp passes, [5] passes x Larmor order lrm,
+ *     [6] sum lrm, [7] sum lrm^2 (one warm alpha per RHS evaluation);
+ *   absorption 0 / 3: [2..7] 0.
+ * stream: hipStream_t or NULL. */
 int torj_trace_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                       const double *N0, const double *weights, int n_psi,
                       const double *psi_grid, double *state, int *status, int *steps,

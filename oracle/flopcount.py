@@ -27,6 +27,10 @@ class Counter:
     n = 0
 
 
+def _real(o):
+    return isinstance(o, (CF, int, float))
+
+
 class CF:
     __slots__ = ("v",)
 
@@ -41,13 +45,15 @@ class CF:
         Counter.n += 1
         return CF(r)
 
-    def __add__(self, o): return self._op(self.v + self._v(o))
+    # other operand types (the complex counting type of flopcount_warm.py) get
+    # their reflected operator: NotImplemented
+    def __add__(self, o): return self._op(self.v + self._v(o)) if _real(o) else NotImplemented
     def __radd__(self, o): return self._op(self._v(o) + self.v)
-    def __sub__(self, o): return self._op(self.v - self._v(o))
+    def __sub__(self, o): return self._op(self.v - self._v(o)) if _real(o) else NotImplemented
     def __rsub__(self, o): return self._op(self._v(o) - self.v)
-    def __mul__(self, o): return self._op(self.v * self._v(o))
+    def __mul__(self, o): return self._op(self.v * self._v(o)) if _real(o) else NotImplemented
     def __rmul__(self, o): return self._op(self._v(o) * self.v)
-    def __truediv__(self, o): return self._op(self.v / self._v(o))
+    def __truediv__(self, o): return self._op(self.v / self._v(o)) if _real(o) else NotImplemented
     def __rtruediv__(self, o): return self._op(self._v(o) / self.v)
     def __neg__(self): return CF(-self.v)
     def __lt__(self, o): return self.v < self._v(o)

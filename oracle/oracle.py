@@ -55,6 +55,8 @@ def lib():
         L.or_spl1d_deriv.restype = C.c_double
         L.or_spl2d_eval.restype = C.c_double
         L.or_spl2d_eval.argtypes = [C.c_void_p, C.c_double, C.c_double]
+        L.or_alpha_warm.restype = C.c_double
+        L.or_expei.restype = C.c_double
         _lib = L
     return _lib
 
@@ -63,9 +65,13 @@ _ALPHA_FN = C.CFUNCTYPE(C.c_double, *([C.c_double] * 7), C.c_int, C.c_int)
 _warm_hook = None
 
 
-def _install_warm_hook():
-    """or_set_alpha_hook -> warm_ref.alpha_warm (absorption models 2 / 3)."""
+def _install_warm_hook(on):
+    """on: or_set_alpha_hook -> warm_ref.alpha_warm (absorption models 2 / 3 through
+    the numpy restatement, serial); off: the C restatement or_alpha_warm."""
     global _warm_hook
+    if not on:
+        lib().or_set_alpha_hook(None)
+        return
     if _warm_hook is None:
         import warm_ref
 
@@ -74,7 +80,26 @@ def _install_warm_hook():
                                        1 if model == 2 else 3)[0]
 
         _warm_hook = _ALPHA_FN(fn)
-        lib().or_set_alpha_hook(_warm_hook)
+    lib().or_set_alpha_hook(_warm_hook)
+
+
+def alpha_warm(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode, iwarm=3):
+    """or_alpha_warm (oracle/torj_warm_oracle.c): (alpha, N_perp_warm^2 complex)."""
+    n2 = np.zeros(2)
+    a = lib().or_alpha_warm(C.c_double(omega), C.c_double(X), C.c_double(Y), C.c_double(N_abs),
+                            C.c_double(N_par), C.c_double(Te), C.c_double(inv_dDdN),
+                            C.c_int(mode), C.c_int(iwarm), _p(n2))
+    return a, complex(n2[0], n2[1])
+
+
+def expei(x):
+    return lib().or_expei(C.c_double(x))
+
+
+def zetac(x, y):
+    out = np.zeros(2)
+    lib().or_zetac(C.c_double(x), C.c_double(y), _p(out))
+    return complex(out[0], out[1])
 
 
 def _p(a):
@@ -194,12 +219,10 @@ class OraclePlasma:
             return 0.0
         if model == 1:
             return self.alpha_approx(x, N, omega, mode)
-        import warm_ref
-
         X, Y, Npar, _ = self.eval_plasma(x, N, omega)
-        return warm_ref.alpha_warm(omega, X, Y, float(np.linalg.norm(N)), Npar, self.T_e(x),
-                                   1.0 / self.grad_norm(x, N, omega, mode), mode,
-                                   1 if model == 2 else 3)[0]
+        return alpha_warm(omega, X, Y, float(np.linalg.norm(N)), Npar, self.T_e(x),
+                          1.0 / self.grad_norm(x, N, omega, mode), mode,
+                          1 if model == 2 else 3)[0]
 
     def alpha_approx(self, x, N, omega, mode):
         return lib().or_alpha_approx(self.ref, _p(_c(x)), _p(_c(N)), C.c_double(omega),
@@ -215,7 +238,7 @@ class OraclePlasma:
     def trace(self, x0, N0, omega, mode, ds, n_steps, chunk_steps=None, psi_exit=1.0,
               P_min=1e-6, absorption=True, psi_grid=None, weights=None, traj_stride=0,
               n_threads=None, samples=False, integrator=0, abstol=1e-6, reltol=1e-6, s_max=None,
-              n_chunks=100, s0=None):
+              n_chunks=100, s0=None, warm="c"):
         """Fixed-step RK4 trace of rays (x0, N0: (n, 3) entry states).  samples=True
         adds "samples": (n, n_steps+1, 3) = (psi_k, dP/ds_k, s_k) at the entry point and
         every step (make_ray's psi / dP_ds vectors, src/solve.jl:151,171).
@@ -241,9 +264,12 @@ class OraclePlasma:
         traj = np.full((n, max(n_save, 1), 5), np.nan)
         w = _c(weights) if weights is not None else None
         nt = n_threads or default_threads()
-        if int(absorption) >= 2:  # warm alpha from warm_ref via a callback: serial
-            _install_warm_hook()
-            nt = 1
+        if int(absorption) >= 2:
+            # warm alpha: the C restatement, multi-threaded; warm="numpy" routes it
+            # through warm_ref.py by a callback instead (serial)
+            _install_warm_hook(warm == "numpy")
+            if warm == "numpy":
+                nt = 1
         smp = np.zeros((n, n_steps + 1, 3)) if samples else None
         lib().or_trace_samples(self.ref, C.byref(cfg), n, _p(x0), _p(N0),
                                _p(w) if w is not None else None, _p(state),

@@ -1134,8 +1134,9 @@ int or_ray_entry(const or_plasma *p, const double x0[3], const double N0[3], dou
 /* ------------------------------------------------------------------------- */
 /* trace: fixed-step RK4 of sys! (src/solve.jl:112-114) + deposition          */
 /* ------------------------------------------------------------------------- */
-/* warm absorption (models 2 and 3) is supplied by the caller: the checker is
- * oracle/warm_ref.py's numpy restatement of src/general_absorption.jl */
+/* warm absorption (models 2 and 3): or_alpha_warm (torj_warm_oracle.c), or,
+ * when the harness installs one, a hook (oracle/warm_ref.py's numpy restatement
+ * of src/general_absorption.jl, serial) */
 static or_alpha_fn g_alpha_hook = NULL;
 
 void or_set_alpha_hook(or_alpha_fn fn) { g_alpha_hook = fn; }
@@ -1146,12 +1147,14 @@ static double alpha_model(const or_plasma *p, const double u[6], double omega, i
                           int model) {
     if (model == 0) return 0.0;
     if (model == 1) return or_alpha_approx(p, u, u + 3, omega, mode);
-    if (!g_alpha_hook) return NAN;
     double X, Y, Npar, b[3];
     or_eval_plasma(p, u, u + 3, omega, &X, &Y, &Npar, b);
     const double Nabs = sqrt(u[3] * u[3] + u[4] * u[4] + u[5] * u[5]);
-    return g_alpha_hook(omega, X, Y, Nabs, Npar, or_T_e(p, u),
-                        1.0 / or_grad_norm(p, u, u + 3, omega, mode), mode, model);
+    const double inv = 1.0 / or_grad_norm(p, u, u + 3, omega, mode);
+    if (g_alpha_hook)
+        return g_alpha_hook(omega, X, Y, Nabs, Npar, or_T_e(p, u), inv, mode, model);
+    return or_alpha_warm(omega, X, Y, Nabs, Npar, or_T_e(p, u), inv, mode, model == 2 ? 1 : 3,
+                         NULL);
 }
 
 static void rhs(const or_plasma *p, const double u[6], double omega, int mode, int absorb,

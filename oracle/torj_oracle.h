@@ -109,8 +109,16 @@ double or_alpha_approx(const or_plasma *p, const double x[3], const double N[3],
 /* |dD/dN| (the gradLambda normalisation, src/solve.jl:85-95) */
 double or_grad_norm(const or_plasma *p, const double x[3], const double N[3], double omega,
                     int mode);
-/* warm alpha for absorption models 2 / 3 (iwarm 1 / 3): (omega, X, Y, N_abs,
- * N_par, Te, 1/|dD/dN|, mode, model) -> alpha; supplied by the test harness */
+/* warm alpha for absorption models 2 / 3 (iwarm 1 / 3), torj_warm_oracle.c:
+ * the repaired src/general_absorption.jl:1328-1337 as oracle/warm_ref.py states
+ * it; N_perp_warm^2 (re, im) into n2 when n2 != NULL */
+double or_alpha_warm(double omega, double X, double Y, double N_abs, double N_par, double Te,
+                     double inv_dDdN, int mode, int iwarm, double *n2);
+double or_expei(double x);                      /* e^-x Ei(x), :29-232 */
+void or_zetac(double x, double y, double out[2]); /* Z(x + iy), TOMS 680, :345-465 */
+/* optional override of models 2 / 3 in the trace: (omega, X, Y, N_abs, N_par,
+ * Te, 1/|dD/dN|, mode, model) -> alpha (the harness's numpy cross-check; NULL
+ * restores or_alpha_warm) */
 typedef double (*or_alpha_fn)(double, double, double, double, double, double, double, int, int);
 void or_set_alpha_hook(or_alpha_fn fn);
 
@@ -137,7 +145,7 @@ typedef struct {
     int chunk_steps;
     double psi_exit;
     double P_min;
-    int absorption;          /* 0 none, 1 Albajar, 2 / 3 warm (or_set_alpha_hook) */
+    int absorption;          /* 0 none, 1 Albajar, 2 / 3 warm (or_alpha_warm) */
     int n_psi;               /* 0: no deposition */
     const double *psi_grid;  /* n_psi */
     int traj_stride;         /* 0: no trajectory */

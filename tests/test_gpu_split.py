@@ -100,7 +100,7 @@ def test_split_counters_match_fused(gpu, T, hplasma):
         state = torch.empty((7, n), dtype=torch.float64, device=dev)
         st = torch.empty(n, dtype=torch.int32, device=dev)
         k = torch.empty(n, dtype=torch.int32, device=dev)
-        cnt = torch.zeros(6, dtype=torch.int64, device=dev)
+        cnt = torch.zeros(8, dtype=torch.int64, device=dev)
         cfg = T._lib.TraceCfg(om, 1, 1e-4, 1500, 15, 1.0, 1e-6, 1, 0)
         stream = torch.cuda.current_stream(dev)
         hplasma.set_sched(sched, 0)

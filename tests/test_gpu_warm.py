@@ -95,7 +95,8 @@ def _x2_rays(T, hplasma, n_rings=2, min_az=3):
 def test_warm_trace_matches_oracle(gpu, T, hplasma, oplasma, model, tol_tau):
     """X2 fan through the 92.5 GHz resonance: RK4 with the warm alpha at every
     stage (solve.jl:112-114 with general_absorption's alpha) vs the C oracle's RK4
-    calling warm_ref per stage."""
+    with its C warm alpha (oracle/torj_warm_oracle.c, pinned to warm_ref.py by
+    tests/test_warm_oracle_c.py)."""
     pos, xp, Np, s0, w, om = _x2_rays(T, hplasma)
     xp, Np = xp[:3], Np[:3]
     kw = dict(ds=1e-3, n_steps=400, chunk_steps=20)

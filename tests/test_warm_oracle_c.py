@@ -1,0 +1,136 @@
+"""Pin the C restatement of the warm absorption (oracle/torj_warm_oracle.c,
+or_alpha_warm: absorption models 2 / 3 of the oracle's multi-threaded trace and
+the all-core CPU peer of bench.py's C5 line) against oracle/warm_ref.py, the
+numpy restatement that tests/test_warm_oracle.py pins to the cold limit, to
+scipy and to the Albajar model.
+
+Tolerances (written per test):
+  * expei (e^-x Ei(x), series / E1 continued fraction / asymptotic series) vs
+    mpmath at 40 digits: 1e-14 relative, 1e-16 absolute near Ei's root x0 = 0.3725;
+  * zetac (TOMS 680, the reference's own algorithm) vs scipy's wofz: 1e-13;
+  * point alpha vs warm_ref, iwarm 3: N_perp^2 and alpha <= 1e-10 (the C and numpy
+    t-quadratures differ only in summation order and expei's last bits);
+    iwarm 1 at Te >= 1 keV: 1e-7 -- the fsup recursion's conditioning (see
+    tests/test_gpu_warm.py), where ACM 680 and scipy's wofz differ in the last bits;
+  * traces: the C alpha vs the numpy callback on the X2 fan ray, same RK4: x, N
+    1e-12 relative, tau 1e-10 relative; the trace is bitwise independent of the
+    thread count.
+"""
+import math
+import warnings
+
+import numpy as np
+import pytest
+
+C_LIGHT = 2.99792458e8
+
+
+def test_expei_vs_mpmath(O):
+    mp = pytest.importorskip("mpmath")
+    mp.mp.dps = 40
+    xs = np.concatenate([-np.logspace(-8, 2.84, 120), np.logspace(-8, 2.84, 120),
+                         [-1.0, -1.0001, 1.0, 39.99, 40.0, 40.0001, 0.3725, 0.3726]])
+    for x in xs:
+        t = float(mp.ei(float(x)) * mp.exp(-float(x)))
+        got = O.expei(float(x))
+        assert abs(got - t) <= 1e-14 * abs(t) + 1e-16, (x, got, t)
+    assert O.expei(0.0) == -1.79e308  # the reference's -xinf (:29-60)
+    for x in (800.0, -800.0):  # warm_ref's 30-term asymptote beyond |x| = 700
+        import warm_ref as W
+
+        assert O.expei(x) == pytest.approx(float(W.expei(np.array([x]))[0]), rel=1e-15)
+
+
+def test_zetac_vs_wofz(O):
+    from scipy.special import wofz
+
+    rng = np.random.default_rng(3)
+    n = 3000
+    xs = rng.uniform(-30, 30, n) * rng.uniform(0, 1, n) ** 3
+    ys = np.abs(rng.uniform(-30, 30, n)) * rng.uniform(0, 1, n) ** 3
+    for x, y in zip(np.append(xs, [0.0, 5.0, -5.0, 0.0]), np.append(ys, [0.0, 0.0, 0.0, 3.0])):
+        ref = 1j * math.sqrt(math.pi) * wofz(complex(x, y))
+        assert abs(O.zetac(x, y) - ref) <= 1e-13 * abs(ref), (x, y)
+
+
+def _sweep(O, n, seed, mode, te_lo):
+    """the point sweep of tests/test_gpu_warm.py"""
+    rng = np.random.default_rng(seed)
+    om = np.full(n, 2 * np.pi * 140e9)
+    X = rng.uniform(0.05, 0.9, n)
+    Y = rng.uniform(0.3, 1.4, n)
+    Npar = rng.uniform(-0.5, 0.5, n)
+    Te = 10 ** rng.uniform(math.log10(te_lo), 4.3, n)
+    inv = rng.uniform(0.2, 2.0, n)
+    N2 = np.array([float(O.refractive_index_sq(x, y, p, mode)) for x, y, p in zip(X, Y, Npar)])
+    Nabs = np.sqrt(np.maximum(N2, Npar ** 2 + 1e-3))
+    return om, X, Y, Nabs, Npar, Te, inv
+
+
+@pytest.mark.parametrize("mode", [1, -1])
+@pytest.mark.parametrize("iwarm,te_lo,tol", [(3, 10.0, 1e-10), (1, 1e3, 1e-7)])
+def test_alpha_warm_c_matches_numpy(O, mode, iwarm, te_lo, tol):
+    import warm_ref as W
+
+    n = 96 if iwarm == 3 else 256  # iwarm 1: the GPU test's 256 points
+    args = _sweep(O, n, 7 + iwarm, mode, te_lo)
+    a, n2 = np.zeros(n), np.zeros(n, complex)
+    ar, nr, conv = np.zeros(n), np.zeros(n, complex), np.zeros(n, bool)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        for i in range(n):
+            pt = [v[i] for v in args]
+            a[i], n2[i] = O.alpha_warm(*pt, mode, iwarm)
+            info = {}
+            ar[i], anpr = W.alpha_warm(*pt, mode, iwarm, info)
+            nr[i], conv[i] = anpr * anpr, info["converged"]
+    assert conv.sum() > 0.8 * n
+    # unconverged points: the same iterate family, not compared (test_gpu_warm.py)
+    both0 = (nr == 0) & (n2 == 0)
+    e_n = np.where(both0, 0.0, np.abs(n2 - nr) / np.maximum(np.abs(nr), 1e-300))
+    floor = 1e-9 * 2 * np.abs(nr) * args[0] / C_LIGHT * args[6]
+    e_a = np.abs(a - ar) / (np.abs(ar) + floor + 1e-300)
+    assert e_n[conv].max() <= tol, e_n[conv].max()
+    assert e_a[conv].max() <= tol, e_a[conv].max()
+
+
+def _x2_ray(O, oplasma):
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    N0 = O.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    om = 2 * np.pi * s["f_abs_test"]
+    st, xp, Np, _ = oplasma.ray_entry([s["R0"], 0.0, s["z0"]], N0, om, 1)
+    assert st == 0
+    return xp[None], Np[None], om
+
+
+@pytest.mark.parametrize("model", [3, 2])
+def test_warm_trace_c_matches_numpy(O, oplasma, model):
+    """the X2 central ray through the 92.5 GHz resonance, RK4 ds = 1 mm:
+    or_alpha_warm in the trace vs warm_ref.alpha_warm through the callback."""
+    xp, Np, om = _x2_ray(O, oplasma)
+    kw = dict(chunk_steps=20, absorption=model, traj_stride=20)
+    c = oplasma.trace(xp, Np, om, 1, 1e-3, 300, **kw)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        p = oplasma.trace(xp, Np, om, 1, 1e-3, 300, warm="numpy", **kw)
+    assert np.array_equal(c["status"], p["status"]) and np.array_equal(c["steps"], p["steps"])
+    sc, sp = c["state"][0], p["state"][0]
+    assert sp[6] > 1.0  # crosses the X2 layer
+    for cols in (slice(0, 3), slice(3, 6)):
+        assert np.abs(sc[cols] - sp[cols]).max() <= 1e-12 * np.linalg.norm(sp[cols])
+    assert abs(sc[6] - sp[6]) <= 1e-10 * sp[6]
+
+
+def test_warm_trace_threads_bitwise(O, oplasma):
+    """the C warm alpha is reentrant: 1 and 4 threads give the same bits."""
+    xp, Np, om = _x2_ray(O, oplasma)
+    off = np.array([[0.0, 0.0, 0.0], [0.0, 0.0, 2e-3], [0.0, 0.0, -2e-3], [0.0, 0.0, 4e-3]])
+    xs, Ns = xp + off, np.repeat(Np, 4, 0)
+    kw = dict(chunk_steps=20, absorption=2, psi_grid=np.linspace(0, 1, 50),
+              weights=np.full(4, 0.25))
+    a = oplasma.trace(xs, Ns, om, 1, 1e-3, 200, n_threads=1, **kw)
+    b = oplasma.trace(xs, Ns, om, 1, 1e-3, 200, n_threads=4, **kw)
+    for k in ("state", "status", "steps", "Pdep"):
+        assert np.array_equal(a[k], b[k]), k

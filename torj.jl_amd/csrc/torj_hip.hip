@@ -394,6 +394,8 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
     const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
     const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
     const unsigned long long s5 = wave_sum((unsigned long long)work.n_zero);
+    const unsigned long long s6 = wave_sum((unsigned long long)work.n_l);
+    const unsigned long long s7 = wave_sum((unsigned long long)work.n_l2);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(a.counters + 0, s0);
         atomicAdd(a.counters + 1, s1);
@@ -401,6 +403,8 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
         atomicAdd(a.counters + 3, s3);
         atomicAdd(a.counters + 4, s4);
         atomicAdd(a.counters + 5, s5);
+        atomicAdd(a.counters + 6, s6);
+        atomicAdd(a.counters + 7, s7);
     }
 }
 
@@ -411,7 +415,7 @@ template <int ABS, int DEPO, bool TRAJ, int LPR = 1>
 __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs a) {
     const int gt = blockIdx.x * blockDim.x + threadIdx.x;
     const int i = gt / LPR, sub = gt % LPR;
-    AlbajarWork work = {0u, 0u, 0u};
+    AlbajarWork work = {};
     unsigned long long steps = 0;
     if (i < a.n) {
         RayState r;
@@ -742,7 +746,7 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
                                                                      unsigned long long *slots,
                                                                      unsigned S, int G, int cs) {
     extern __shared__ double lds_k[];  // integrator 1: Tsit5 stage vectors of this wave
-    AlbajarWork work = {0u, 0u, 0u};
+    AlbajarWork work = {};
     unsigned long long steps = 0, nrhs = 0;
     double *hist = lds_k + a.hist_off;  // binned deposition: this wave's shell histogram
     if constexpr (DEPO == kDepoBinned) {
@@ -1072,7 +1076,7 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     const int ti = sp.tinfo[i];
     if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
     const double *in = sp.ain + (size_t)js * kAinF * a.n + i;
-    AlbajarWork work = {0u, 0u, 0u};
+    AlbajarWork work = {};
     const double al = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
         c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
         in[4 * (size_t)a.n], a.mode, &work);

@@ -658,11 +658,15 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     return s;
 }
 
+// Work counters of one lane (include/torj_hip.h torj_trace: counters[2..7]).
+// Albajar (ABS 1) / warm weakly relativistic (ABS 2, torj_warm.hpp) meaning:
 struct AlbajarWork {
-    uint32_t n_active;  // calls that reached the harmonic loop
-    uint32_t n_harm;    // harmonic integrals evaluated (node loop run)
-    uint32_t n_terms;   // Bessel-series terms evaluated (sum over node pairs of K)
-    uint32_t n_zero;    // harmonic integrals found exactly zero without the node loop
+    uint32_t n_active;  // calls that reached the harmonic loop / larmornumber tests
+    uint32_t n_harm;    // harmonic integrals evaluated (node loop run) / Faddeeva evaluations
+    uint32_t n_terms;   // Bessel-series terms (sum over node pairs of K) / warmdisp passes
+    uint32_t n_zero;    // harmonic integrals found exactly zero / passes x Larmor order
+    uint32_t n_l;       // - / sum of Larmor orders lrm
+    uint32_t n_l2;      // - / sum of lrm^2
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +

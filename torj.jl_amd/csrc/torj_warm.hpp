@@ -418,11 +418,12 @@ TORJ_HD void tensor_store(Tensor<L> &T, int l, double xg, double fl, const cplx 
 // m[ir] = cefm(isa, ir), ir = 0..2, summed over is = -isa then +isa in the
 // reference's order.  Only the last three steps of the l-recurrence are
 // stored, so p / m are indexed statically and stay in registers.
-TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
+TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
     const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
     const bool big_psi = apsi > 0.7;
     const double ipsi2 = big_psi ? 1.0 / (psi * psi) : 0.0, i2psi = big_psi ? 0.5 / psi : 0.0;
     for (int ir = 0; ir < 3; ir++) p[ir] = m[ir] = C(0.0);
+    int nfad = 0;  // Faddeeva evaluations (the work counters, torj_hip/flops.py)
     for (int sg = (isa == 0 ? 1 : -1); sg <= 1; sg += 2) {
         const int is = sg * isa;
         const double alpha = anpl2hm1 + is * yg, phi2 = amu * alpha, phim = sqrt(fabs(phi2));
@@ -440,6 +441,7 @@ TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx
         cplx czp, czm, cz0;
         const bool mirror = alpha < 0;
         const int nz = big_psi ? 2 : 3;
+        nfad += nz - (mirror ? 1 : 0);
 #pragma unroll 1
         for (int kz = 0; kz < nz; kz++) {
             if (kz == 1 && mirror) continue;
@@ -484,22 +486,24 @@ TORJ_HD void fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx
             m[ir] = is > 0 ? m[ir] + cf2 : m[ir] - cf2;
         }
     }
+    return nfad;
 }
 
 // weakly relativistic tensor (fsup + dieltens_maxw_wr, :473-638).  The |s|
 // loop runs outermost and adds its terms to every l >= |s|, in the
 // reference's summation order; ca[l][.] is indexed statically (registers).
 template <int L>
-TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor<L> &T) {
+TORJ_HD int dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor<L> &T) {
     const double anpl2 = anpl * anpl;
     cplx ca[L][6];
 #pragma unroll
     for (int l = 0; l < L; l++)
         for (int q = 0; q < 6; q++) ca[l][q] = C(0.0);
     cplx p0[3];
+    int nfad = 0;
     for (int isa = 0; isa <= lrm; isa++) {
         cplx p[3], m[3];
-        fsup_s(yg, anpl, amu, isa, p, m);
+        nfad += fsup_s(yg, anpl, amu, isa, p, m);
         if (isa == 0) p0[0] = p[0], p0[1] = p[1], p0[2] = p[2];
         const double is = isa;
         const cplx cq0p = amu * p[0], cq0m = amu * m[0];
@@ -529,6 +533,7 @@ TORJ_HD void dieltens_wr(double xg, double yg, double anpl, double amu, int lrm,
     }
     const cplx cq2p = p0[1] + amu * anpl2 * (p0[2] + p0[0] - 2.0 * p0[1]);
     T.e330 = 1.0 - xg * amu * cq2p;
+    return nfad;
 }
 
 // fully relativistic tensor (hermitian iwarm > 2 + antihermitian +
@@ -671,11 +676,13 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
 // warmdisp (:1158-1267) -> N_perp^2 (complex); anpr2 initialised (R2)
 template <int L>
 TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int sox, int lrm,
-                          const Tensor<L> &T) {
+                          const Tensor<L> &T, int &passes) {
     cplx anpr2a = C(anprc * anprc), anpr2 = anpr2a;
     const double anpl2 = anpl * anpl;
     double errnpr = 1.0;
+    passes = 0;  // tensor sums evaluated (the work counters)
     for (int i = 1; i <= 100; i++) {
+        passes = i;
         cplx s[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
         cplx pw = C(1.0);
 #pragma unroll
@@ -710,13 +717,15 @@ TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int so
     return anpr2;
 }
 
-// larmornumber (:1285-1326)
-TORJ_HD int larmornumber(double yg, double npl, double mu) {
+// larmornumber (:1285-1326); trips = resonance tests made (the work counters)
+TORJ_HD int larmornumber(double yg, double npl, double mu, int &trips) {
     const double dnl = 1.0 - npl * npl;
     int imax = 1;
     int nharm = (int)floor(1.0 / yg);
     if (nharm * yg < 1.0) nharm++;
+    trips = 0;
     for (;;) {
+        trips++;
         const double ygn = nharm * yg, rdu2 = ygn * ygn - dnl;
         const double gg = (ygn - sqrt(npl * npl * rdu2)) / dnl;
         if (mu * (gg - 1.0) > 15.0) break;
@@ -728,6 +737,10 @@ TORJ_HD int larmornumber(double yg, double npl, double mu) {
         }
     }
     return nharm;
+}
+TORJ_HD int larmornumber(double yg, double npl, double mu) {
+    int trips;
+    return larmornumber(yg, npl, mu, trips);
 }
 
 // alpha (:1328-1337): iwarm 1 (weakly relativistic) or 3 (fully relativistic,
@@ -752,21 +765,25 @@ TORJ_HD int larmornumber(double yg, double npl, double mu) {
 struct WarmAlpha {
     double alpha;
     cplx n2;
+    // trip counts of the data-dependent loops (iwarm 1: Faddeeva evaluations;
+    // both: warmdisp passes, Larmor order, larmornumber tests) -> torj_hip/flops.py
+    int nfad, passes, lrm, ltrips;
 };
 template <int IWARM, int L>
 TORJ_HD WarmAlpha alpha_core(double omega, double X, double Y, double N_par, double mu, double npr,
                              int lrm, double inv_dDdN, int mode) {
     Tensor<L> T;
+    int nfad = 0, passes;
     if constexpr (IWARM == 1)
-        dieltens_wr<L>(X, Y, N_par, mu, lrm, T);
+        nfad = dieltens_wr<L>(X, Y, N_par, mu, lrm, T);
     else
         dieltens_fr<L>(X, Y, N_par, mu, lrm, T);
     // identity on the l = 1 diagonal (:629-630 / :1125-1126)
     T.e[0][0] = T.e[0][0] + 1.0;
     T.e[0][2] = T.e[0][2] + 1.0;
     const int sox = Y <= 1.0 ? mode : -mode;
-    const cplx a2 = warmdisp_n2<L>(X, Y, N_par, npr, sox, lrm, T);
-    return {2.0 * a2.im * omega / kC * inv_dDdN, a2};
+    const cplx a2 = warmdisp_n2<L>(X, Y, N_par, npr, sox, lrm, T, passes);
+    return {2.0 * a2.im * omega / kC * inv_dDdN, a2, nfad, passes, lrm, 0};
 }
 
 // The tensor is sized for lrm <= 3 (the common case: one to three Larmor
@@ -777,15 +794,18 @@ TORJ_WARM_ATTR WarmAlpha alpha_warm_v(double omega, double X, double Y, double N
                                       double Te, double inv_dDdN, int mode) {
     const double mu = kMe * kC * kC / (Te * kE);
     const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
-    const int nharm = larmornumber(Y, N_par, mu);
+    int ltrips;
+    const int nharm = larmornumber(Y, N_par, mu, ltrips);
     const int lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
 #if defined(__HIP_DEVICE_COMPILE__)
     const bool big = __ballot(lrm > 3) != 0;
 #else
     const bool big = lrm > 3;
 #endif
-    return big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode)
-               : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode);
+    WarmAlpha r = big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode)
+                      : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode);
+    r.ltrips = ltrips;
+    return r;
 }
 
 template <int IWARM>
@@ -820,8 +840,17 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
         alpha = abs_albajar_fast<LPR>(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, sub);
     } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = alpha_warm_t<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode,
-                                               nullptr);
+        const WarmAlpha r =
+            alpha_warm_v<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode);
+        alpha = r.alpha;
+        if (ABS == 2 && work) {  // the weakly relativistic op count's trips (flops.py)
+            work->n_active += r.ltrips;
+            work->n_harm += r.nfad;
+            work->n_terms += r.passes;
+            work->n_zero += r.passes * r.lrm;
+            work->n_l += r.lrm;
+            work->n_l2 += r.lrm * r.lrm;
+        }
     } else {
         alpha = 0.0;
     }

@@ -92,7 +92,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 3  # include/torj_hip.h TORJ_ABI_VERSION
+ABI_VERSION = 4  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 

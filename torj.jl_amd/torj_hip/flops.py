@@ -35,3 +35,38 @@ def algorithmic_flops(counters, n_gl: int = 24) -> float:
             + harm * (FLOPS_HARM + pairs * FLOPS_PAIR_SHARED + n_gl * FLOPS_NODE)
             + zero * (FLOPS_HARM + FLOPS_ZERO_TEST)
             + FLOPS_SERIES_TERM * (terms - harm * pairs))
+
+
+# Weakly relativistic warm alpha (absorption 2, torj_warm.hpp alpha_warm_v<1>),
+# per trip, from the instrumented restatement `python oracle/flopcount_warm.py`
+# (same convention; factorial tables and loop invariants not counted; branch-
+# dependent parts at their cheapest branch, so the model is a lower bound: 97.5-
+# 99.8 % of the instrumented count, tests/test_warm_flops.py).
+FLOPS_WARM_CALL = 77          # Te, |N|, mu, N_perp, per-call invariants, e330, alpha
+FLOPS_WARM_LARMOR_TEST = 10   # per larmornumber resonance test
+FLOPS_WARM_FADDEEVA = 278     # per Z(z): Weideman N = 36 complex Horner sum
+FLOPS_WARM_SIDE = 14          # per fsup side s = +-|s|: alpha_s, phi, cf12, cf32
+FLOPS_WARM_STEP = 6           # per Shkarofsky recursion step
+FLOPS_WARM_STORE = 4          # per stored recursion step: cefp, cefm accumulation
+FLOPS_WARM_ISA = 22           # per |s|: cq0p .. cq2p
+FLOPS_WARM_PAIR = 27          # per (|s|, l) term of the tensor sums
+FLOPS_WARM_ORDER = 15         # per Larmor order l: f_l and the six components
+FLOPS_WARM_SUM_TERM = 54      # per warmdisp pass and order: sum eps_l N_perp^(2l)
+FLOPS_WARM_UPDATE = 168       # per warmdisp update: cc4, cc2, cc0, root, convergence
+
+
+def algorithmic_flops_warm(counters) -> float:
+    """counters = the 8 work counters of an absorption-2 launch (include/torj_hip.h
+    torj_trace_device): ray-steps, RHS evaluations (= warm alpha calls), larmornumber
+    tests, Faddeeva evaluations, warmdisp passes, passes x lrm, sum lrm, sum lrm^2."""
+    steps, calls, tests, fad, passes, pass_l, sl, sl2 = (float(c) for c in counters[:8])
+    sides = 2.0 * sl + calls                  # is = -|s| .. |s|
+    rsteps = sl2 + 5.0 * sl + 2.0 * calls     # recursion steps: lrm^2 + 5 lrm + 2 per call
+    stored = 6.0 * sl + 2.0 * calls
+    pairs = 0.5 * (sl2 + 3.0 * sl)            # (|s|, l), max(|s|, 1) <= l <= lrm
+    updates = passes - calls                  # every pass but the breaking one
+    return (steps * FLOPS_STEP_OVERHEAD + calls * (FLOPS_RHS_COLD + FLOPS_WARM_CALL)
+            + tests * FLOPS_WARM_LARMOR_TEST + fad * FLOPS_WARM_FADDEEVA
+            + sides * FLOPS_WARM_SIDE + rsteps * FLOPS_WARM_STEP + stored * FLOPS_WARM_STORE
+            + (sl + calls) * FLOPS_WARM_ISA + pairs * FLOPS_WARM_PAIR + sl * FLOPS_WARM_ORDER
+            + pass_l * FLOPS_WARM_SUM_TERM + updates * FLOPS_WARM_UPDATE)
