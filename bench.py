@@ -470,6 +470,9 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
                   "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
                   "max_rel_tau_unfloored": float(et_strict.max()),
                   "max_rel": float(max(ex.max(), eN.max(), et.max())),
+                  "worst_tau_ray": {"fan_index": int(idx[int(et.argmax())]),
+                                    "tau_gpu": float(gs[int(et.argmax()), 6]),
+                                    "tau_cpu": float(os_[int(et.argmax()), 6])},
                   "bar": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)}
     what = ("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
             else "oracle/torj_oracle.c OpenMP")
