@@ -287,6 +287,8 @@ def main():
                 "hbm_GBps": traffic["traffic_bytes"] / kern_s / 1e9 if traffic else None,
                 "hbm_frac": traffic["traffic_bytes"] / kern_s / HBM_PEAK_BPS if traffic else None,
                 "valu_busy": traffic.get("valu_busy") if traffic else None,
+                "valu_busy_by_kernel": traffic.get("valu_busy_by_kernel") if traffic else None,
+                "valu_active_per_wave": traffic.get("valu_active_per_wave") if traffic else None,
                 # executed fp64 FLOPs of the same kernel and workload (PMC:
                 # SQ_INSTS_VALU_{FMA,MUL,ADD,TRANS}_F64 x 64 lanes, FMA x 2)
                 "executed_TFLOPs": (traffic["fp64_flops_executed"] / kern_s / 1e12
@@ -386,11 +388,22 @@ def measured_traffic(kname, n, args):
                 and wl.get("traj_stride") == args.traj_stride
                 and wl.get("absorption", "albajar") == args.absorption):
             t["file"] = os.path.relpath(f, ROOT)
-            # VALU-busy of the same profile: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES
-            # (fraction of the hot kernel's wave-cycles issuing VALU)
+            # VALU-busy of the same profile, SIMD level: the quad-cycles the kernel's
+            # waves issued VALU (SQ_ACTIVE_INST_VALU x 4 cycles) over the SIMD-cycles
+            # of its dispatches (GRBM_GUI_ACTIVE is summed over the 8 XCDs; 1024
+            # SIMDs).  Overlapped pipeline dispatches each count the shared wall
+            # cycles, so there the figure is a lower bound; per kernel beside it.
+            # valu_active_per_wave: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES.
+            def simd_busy(c):
+                return 4.0 * c["SQ_ACTIVE_INST_VALU"] / (1024 * c["GRBM_GUI_ACTIVE"] / 8.0)
             try:
-                pmc = json.load(open(f.replace("traffic.json", "pmc_summary.json")))["avg"]
-                t["valu_busy"] = pmc["SQ_ACTIVE_INST_VALU"] / pmc["SQ_WAVE_CYCLES"]
+                summ = json.load(open(f.replace("traffic.json", "pmc_summary.json")))
+                pmc = summ["avg"]
+                t["valu_busy"] = simd_busy(pmc)
+                t["valu_active_per_wave"] = pmc["SQ_ACTIVE_INST_VALU"] / pmc["SQ_WAVE_CYCLES"]
+                if summ.get("by_kernel"):
+                    t["valu_busy_by_kernel"] = {k: simd_busy(v) for k, v in summ["by_kernel"].items()
+                                                if v.get("GRBM_GUI_ACTIVE")}
             except (OSError, ValueError, KeyError, ZeroDivisionError):
                 t["valu_busy"] = None
             if "|" in base:  # pipeline: rocprof's per-launch kernel times of the same workload

@@ -551,21 +551,31 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
     const double bth2 = 2.0 / amu, bth = sqrt(bth2);
     const double amu2 = amu * amu, amu4 = amu2 * amu2, amu6 = amu4 * amu2;
     const double iamu = 1.0 / amu, i2amu = 0.5 * iamu;
-    for (int n = -llm; n <= llm; n++) {
-        const int mlo = n < 0 ? -n : n;
-        double acc[4][3];
-        for (int m = 0; m < 4; m++) acc[m][0] = acc[m][1] = acc[m][2] = 0.0;
-        for (int i = 0; i < kNtv; i++) {
-            const double t = -kTmax + i * kDtv, t2 = t * t;
-            const double rxt = sqrt_pos(fma(t2, i2amu, 1.0)), x = t * rxt;
-            const double upl2 = bth2 * x * x, upl = bth * x, gx = fma(t2, iamu, 1.0);
-            const double exdx = cr * kFrW.w[i] * gx * rcp_nz(rxt);
+    // node-outer: the t-only quantities of node i once for every n (the
+    // reference's n-outer loop recomputes them per n); acc[n + 3][m][k] sums
+    // over i in the same order, statically indexed so it stays in registers
+    double acc[7][4][3];
+#pragma unroll
+    for (int a = 0; a < 7; a++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[a][m][0] = acc[a][m][1] = acc[a][m][2] = 0.0;
+    for (int i = 0; i < kNtv; i++) {
+        const double t = -kTmax + i * kDtv, t2 = t * t;
+        const double rxt = sqrt_pos(fma(t2, i2amu, 1.0)), x = t * rxt;
+        const double upl2 = bth2 * x * x, upl = bth * x, gx = fma(t2, iamu, 1.0);
+        const double exdx = cr * kFrW.w[i] * gx * rcp_nz(rxt);
+#pragma unroll
+        for (int n = -3; n <= 3; n++) {
+            const int mlo = n < 0 ? -n : n;
+            if (mlo > llm) continue;
             const double gr = anpl * upl + n * yg;
             const double zm = -amu * (gx - gr), s = amu * (gx + gr);
             const double fe0m = expei(zm), zm2 = zm * zm;
-            for (int m = mlo; m <= llm; m++) {
+#pragma unroll
+            for (int m = mlo; m <= 3; m++) {
+                if (m > llm) break;
                 if (m == 0) {
-                    acc[0][2] += -exdx * fe0m * upl2;
+                    acc[n + 3][0][2] += -exdx * fe0m * upl2;
                     continue;
                 }
                 double ffe;
@@ -576,13 +586,20 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
                 else
                     ffe = (18.0 * s * (s + 4.0 - zm) + 6.0 * (20.0 - 8.0 * zm + zm2) +
                            s * s * s * (2.0 + zm + zm2 - zm2 * zm * fe0m)) / amu6;
-                acc[m][0] += exdx * ffe;
-                acc[m][1] += exdx * ffe * upl;
-                acc[m][2] += exdx * ffe * upl2;
+                acc[n + 3][m][0] += exdx * ffe;
+                acc[n + 3][m][1] += exdx * ffe * upl;
+                acc[n + 3][m][2] += exdx * ffe * upl2;
             }
         }
-        for (int m = mlo; m <= llm; m++)
-            for (int k = 0; k < 3; k++) rr[n + 3][k][m] = acc[m][k];
+    }
+#pragma unroll
+    for (int n = -3; n <= 3; n++) {
+        const int mlo = n < 0 ? -n : n;
+#pragma unroll
+        for (int m = mlo; m <= 3; m++)
+            if (m <= llm)
+#pragma unroll
+                for (int k = 0; k < 3; k++) rr[n + 3][k][m] = acc[n + 3][m][k];
     }
     // anti-hermitian part ri[n-1][k][m-1], m >= n
     double ri[kWarmMaxL][3][kWarmMaxL];
