@@ -385,11 +385,58 @@ TORJ_HD cplx faddeeva_upper(double x, double y) {
     return w;
 }
 
+// two arguments at once, their Horner chains interleaved (each the same
+// operation sequence as faddeeva_upper, so the same bits): the warm kernels
+// run one wave per SIMD, where a single dependent fp64 chain leaves every
+// other issue slot empty
+TORJ_HD void faddeeva_upper2(double x0, double y0, double x1, double y1, cplx &w0, cplx &w1) {
+    constexpr double kInvSqrtPi = 0.56418958354775628695;
+    const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
+    double ir[2], ii[2], Zr[2], Zi[2], pr[2], pim[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const double dr = kWeidL + ys[q], di = -xs[q];
+        const double id = rcp_nz(fma(dr, dr, di * di));
+        ir[q] = dr * id;
+        ii[q] = -di * id;
+        const double nr = kWeidL - ys[q], ni = xs[q];
+        Zr[q] = fma(nr, ir[q], -ni * ii[q]);
+        Zi[q] = fma(nr, ii[q], ni * ir[q]);
+        pr[q] = kWeidA[0];
+        pim[q] = 0.0;
+    }
+#pragma unroll
+    for (int k = 1; k < kWeidN; k++) {
+#pragma unroll
+        for (int q = 0; q < 2; q++) {
+            const double t = fma(pr[q], Zr[q], fma(-pim[q], Zi[q], kWeidA[k]));
+            pim[q] = fma(pr[q], Zi[q], pim[q] * Zr[q]);
+            pr[q] = t;
+        }
+    }
+    cplx w[2];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const double i2r = fma(ir[q], ir[q], -ii[q] * ii[q]), i2i = 2.0 * ir[q] * ii[q];
+        w[q].re = fma(2.0, fma(pr[q], i2r, -pim[q] * i2i), kInvSqrtPi * ir[q]);
+        w[q].im = fma(2.0, fma(pr[q], i2i, pim[q] * i2r), kInvSqrtPi * ii[q]);
+        if (ys[q] == 0.0) w[q].re = exp(-xs[q] * xs[q]);
+    }
+    w0 = w[0];
+    w1 = w[1];
+}
+
 // Z(z) = i sqrt(pi) w(z) (zetac, :345-465); the warm tensor's arguments all
 // have Im z >= 0 (zetac_upper); TOMS 680 serves Im z < 0
 TORJ_HD cplx zetac_upper(double x, double y) {
     const cplx w = faddeeva_upper(x, y);
     return {-kSqrtPi * w.im, kSqrtPi * w.re};
+}
+TORJ_HD void zetac_upper2(double x0, double y0, double x1, double y1, cplx &z0, cplx &z1) {
+    cplx w0, w1;
+    faddeeva_upper2(x0, y0, x1, y1, w0, w1);
+    z0 = {-kSqrtPi * w0.im, kSqrtPi * w0.re};
+    z1 = {-kSqrtPi * w1.im, kSqrtPi * w1.re};
 }
 TORJ_HD cplx zetac(double x, double y) {
     if (y >= 0.0) return zetac_upper(x, y);
@@ -417,61 +464,68 @@ TORJ_HD void tensor_store(Tensor<L> &T, int l, double xg, double fl, const cplx 
 // Shkarofsky coefficients of one |s| (fsup, :473-561): p[ir] = cefp(isa, ir),
 // m[ir] = cefm(isa, ir), ir = 0..2, summed over is = -isa then +isa in the
 // reference's order.  Only the last three steps of the l-recurrence are
-// stored, so p / m are indexed statically and stay in registers.
+// stored, so p / m are indexed statically and stay in registers.  The two
+// sides' Faddeeva evaluations run as interleaved pairs (zetac_upper2).
 TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
     const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
     const bool big_psi = apsi > 0.7;
     const double ipsi2 = big_psi ? 1.0 / (psi * psi) : 0.0, i2psi = big_psi ? 0.5 / psi : 0.0;
     for (int ir = 0; ir < 3; ir++) p[ir] = m[ir] = C(0.0);
-    int nfad = 0;  // Faddeeva evaluations (the work counters, torj_hip/flops.py)
-    for (int sg = (isa == 0 ? 1 : -1); sg <= 1; sg += 2) {
-        const int is = sg * isa;
-        const double alpha = anpl2hm1 + is * yg, phi2 = amu * alpha, phim = sqrt(fabs(phi2));
-        double xp, yp, xm, ym, x0, y0;
-        if (alpha >= 0) {
-            xp = psi - phim, yp = 0.0, xm = -psi - phim, ym = 0.0, x0 = -phim, y0 = 0.0;
+    // side q = 0: is = -isa, q = 1: is = +isa (isa = 0: side 1 only; side 0
+    // then repeats it as the partner of the pairs, and is not used)
+    double alpha[2], phi2[2], phim[2], zx[2][3], zy[2][3];
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        const int is = q == 0 ? -isa : isa;
+        alpha[q] = anpl2hm1 + is * yg;
+        phi2[q] = amu * alpha[q];
+        phim[q] = sqrt(fabs(phi2[q]));
+        if (alpha[q] >= 0) {
+            zx[q][0] = psi - phim[q], zy[q][0] = 0.0, zx[q][1] = -psi - phim[q], zy[q][1] = 0.0;
+            zx[q][2] = -phim[q], zy[q][2] = 0.0;
         } else {
-            xp = psi, yp = phim, xm = -psi, ym = phim, x0 = 0.0, y0 = phim;
+            zx[q][0] = psi, zy[q][0] = phim[q], zx[q][1] = -psi, zy[q][1] = phim[q];
+            zx[q][2] = 0.0, zy[q][2] = phim[q];
         }
-        // one zetac call site for the two (three) arguments: a single inlined copy
-        // of the Faddeeva code per tensor instance.  Below the resonance
-        // (alpha < 0) z_m = -conj(z_p), and the algorithm's w(-conj z) is
-        // conj(w(z)) bit for bit (it evaluates |x| and flips Im w), so Z(z_m) =
-        // -conj(Z(z_p)) and one evaluation serves both.
-        cplx czp, czm, cz0;
-        const bool mirror = alpha < 0;
-        const int nz = big_psi ? 2 : 3;
-        nfad += nz - (mirror ? 1 : 0);
-#pragma unroll 1
-        for (int kz = 0; kz < nz; kz++) {
-            if (kz == 1 && mirror) continue;
-            const double zx = kz == 0 ? xp : (kz == 1 ? xm : x0);
-            const double zy = kz == 0 ? yp : (kz == 1 ? ym : y0);
-            const cplx z = zetac_upper(zx, zy);  // zy = 0 or phim >= 0
-            if (kz == 0)
-                czp = z;
-            else if (kz == 1)
-                czm = z;
-            else
-                cz0 = z;
-        }
-        if (mirror) czm = C(-czp.re, czp.im);
+    }
+    // Below the resonance (alpha < 0) z_m = -conj(z_p), and the algorithm's
+    // w(-conj z) is conj(w(z)) bit for bit (it evaluates |x| and flips Im w),
+    // so Z(z_m) = -conj(Z(z_p)) and one evaluation serves both.
+    const bool mirror[2] = {alpha[0] < 0, alpha[1] < 0};
+    cplx cz[2][3];
+    zetac_upper2(zx[0][0], zy[0][0], zx[1][0], zy[1][0], cz[0][0], cz[1][0]);
+    if (!big_psi) zetac_upper2(zx[0][2], zy[0][2], zx[1][2], zy[1][2], cz[0][2], cz[1][2]);
+    if (!mirror[0] && !mirror[1]) {
+        zetac_upper2(zx[0][1], zy[0][1], zx[1][1], zy[1][1], cz[0][1], cz[1][1]);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+            cz[q][1] = mirror[q] ? C(-cz[q][0].re, cz[q][0].im) : zetac_upper(zx[q][1], zy[q][1]);
+    }
+    int nfad = 0;  // Faddeeva evaluations of the reference's algorithm (the work counters, torj_hip/flops.py)
+#pragma unroll
+    for (int q = 0; q < 2; q++) {
+        if (q == 0 && isa == 0) continue;
+        const int is = q == 0 ? -isa : isa;
+        nfad += (big_psi ? 2 : 3) - (mirror[q] ? 1 : 0);
+        const cplx czp = cz[q][0], czm = cz[q][1], cz0 = cz[q][2];
         cplx cf12 = C(0.0);
-        if (alpha != 0.0) {
-            const double i2phim = 0.5 * rcp_pos(phim);
-            cf12 = alpha > 0 ? -((czp + czm) * i2phim) : -I_times((czp + czm) * i2phim);
+        if (alpha[q] != 0.0) {
+            const double i2phim = 0.5 * rcp_pos(phim[q]);
+            cf12 = alpha[q] > 0 ? -((czp + czm) * i2phim) : -I_times((czp + czm) * i2phim);
         }
         cplx cf32;
         if (big_psi) {
             cf32 = -((czp - czm) * i2psi);
         } else {
-            const cplx cphi = alpha < 0 ? C(0.0, -phim) : C(phim);
+            const cplx cphi = alpha[q] < 0 ? C(0.0, -phim[q]) : C(phim[q]);
             cf32 = 2.0 * (1.0 - cphi * cz0);
         }
         cplx cf0 = cf12, cf1 = cf32;
+        const double ph2 = phi2[q];
         auto step = [&](int l) {
-            const cplx cf2 = big_psi ? (1.0 + phi2 * cf0 - (l - 0.5) * cf1) * ipsi2
-                                     : (1.0 + phi2 * cf1) * rcp_pos(l + 0.5);
+            const cplx cf2 = big_psi ? (1.0 + ph2 * cf0 - (l - 0.5) * cf1) * ipsi2
+                                     : (1.0 + ph2 * cf1) * rcp_pos(l + 0.5);
             cf0 = cf1;
             cf1 = cf2;
             return cf2;
