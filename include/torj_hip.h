@@ -257,11 +257,13 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
  * trace with 16 lanes per ray (Albajar absorption, no binning: the node pairs
  * of the absorption integral split between a ray's lanes, results equal to
  * rounding; mode -1 picks it for beams of at most 2 x 64 x SIMDs / 16 rays
- * unless env TORJ_LPR=1); 3: the split RK4 path (fixed steps, Albajar): the
- * trajectories' cold RK4 in one kernel, the 4 x n_steps alpha evaluations per
- * ray in a fully parallel one, the optical depth by an in-order scan, blocks of
- * steps pipelined over two streams (mode -1 picks it where it
- * would pick 1, unless env TORJ_SPLIT=0).
+ * unless env TORJ_LPR=1); 3: the split RK4 path (fixed steps, Albajar or
+ * warm absorption): the trajectories' cold RK4 in one kernel, the 4 x n_steps
+ * alpha evaluations per ray in a fully parallel one, the optical depth by an
+ * in-order scan, blocks of steps pipelined over two streams (DESIGN.md 3.7;
+ * mode -1 picks it for Albajar where it would pick 1, and for the warm models
+ * on beams of fewer than 3 x 64-ray groups per CU, unless env TORJ_SPLIT=0;
+ * TORJ_SPLIT_WARM=0 / 1 turns the warm choice off / on for every size).
  * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16));
  * steps per pipeline block for mode 3 (0 = from the 1 GiB per alpha-input
  * buffer budget, env TORJ_SPLIT_MB; four buffers in flight). */

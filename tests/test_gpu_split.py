@@ -132,3 +132,57 @@ def test_split_on_129_grid_vs_oracle(gpu, T, O):
     o = op.trace(xp, Np, om, 1, 1e-4, 2000, psi_grid=grid, weights=w)
     _compare_trace(g, o)
     assert np.abs(g.dP_shell[:-1] - o["dP"]).max() <= 1e-10 * np.abs(o["dP"]).max()
+
+
+@pytest.mark.parametrize("model,n_rings", [(2, 14), (3, 5)])
+def test_split_warm_equals_fused(gpu, T, hplasma, model, n_rings):
+    """The warm models on the split path (k_alpha_warm_pts: the group-velocity
+    factor as a sixth stored input): the library's default for small warm beams
+    (fewer groups than 3 per CU) and sched mode 3, against the fused work-queue
+    kernel: statuses and steps exact, x, N 1e-12, tau 1e-10 (measured 7e-12 /
+    4e-15), reference deposition 1e-9; the iwarm-1 work counters (integer trip
+    counts of the same alpha code) equal."""
+    import ctypes
+
+    import torch
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, n_rings=n_rings)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, absorption=model,
+              psi_grid=np.linspace(0, 1, 500), deposition="reference", x_launch=pos, s0=s0)
+    a = _run(T, hplasma, 1, 0, xp, Np, om, 1, **kw)   # fused work queue
+    b = T.trace(hplasma, xp, Np, om, 1, **kw)           # default: split (small warm beam)
+    c = _run(T, hplasma, 3, 0, xp, Np, om, 1, **kw)   # forced split
+    for r in (b, c):
+        assert np.array_equal(a.status, r.status) and np.array_equal(a.steps, r.steps)
+        for cols in (slice(0, 3), slice(3, 6)):
+            e = np.abs(a.state[:, cols] - r.state[:, cols]).max(1) / np.linalg.norm(a.state[:, cols], axis=1)
+            assert e.max() <= 1e-12, e.max()
+        assert a.state[:, 6].min() > 1.0  # the X2 layer is crossed
+        assert (np.abs(a.state[:, 6] - r.state[:, 6]) / a.state[:, 6]).max() <= 1e-10
+        assert np.abs(a.P_dep - r.P_dep).max() <= 1e-9
+        assert np.abs(a.dP_shell - r.dP_shell).max() <= 1e-9 * np.abs(a.dP_shell).max()
+    if model != 2:
+        return
+    dev = torch.device("cuda", 0)
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    x0, N0, n = t(xp.T), t(Np.T), len(w)
+    out = []
+    for sched in (1, 3):
+        state = torch.empty((7, n), dtype=torch.float64, device=dev)
+        st = torch.empty(n, dtype=torch.int32, device=dev)
+        k = torch.empty(n, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+        cfg = T._lib.TraceCfg(om, 1, 1e-4, 2000, 20, 1.0, 1e-6, 2, 0)
+        stream = torch.cuda.current_stream(dev)
+        hplasma.set_sched(sched, 0)
+        try:
+            T._lib.check(T.lib().torj_trace_device(hplasma.handle, cfg, n, x0.data_ptr(),
+                                                   N0.data_ptr(), None, 0, None, state.data_ptr(),
+                                                   st.data_ptr(), k.data_ptr(), None, None, None,
+                                                   ctypes.c_void_p(cnt.data_ptr()),
+                                                   stream.cuda_stream))
+            T._lib.check(T.lib().torj_trace_check(hplasma.handle, stream.cuda_stream))
+        finally:
+            hplasma.set_sched(-1)
+        out.append(cnt.cpu().numpy())
+    assert np.array_equal(out[0], out[1]), (out[0], out[1])

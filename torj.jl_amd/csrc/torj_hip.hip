@@ -876,13 +876,16 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
 // group at one (step, stage): the same lanes as the fused kernel's wave there,
 // so the per-wave Bessel-level ballot and every alpha are the same bits.
 // ---------------------------------------------------------------------------
-constexpr int kAinF = 5;  // X, Y, |N|, N_par, Te
+constexpr int kAinF = 5;  // X, Y, |N|, N_par, Te (+ 1 / |dD/dN| for the warm alpha: kAinFW)
+constexpr int kAinFW = 6;
 
 struct SplitArgs {
-    double *ain;          // [j][stage][f][n]: this block's alpha inputs
+    double *ain;          // [j][stage][f][n]: this block's alpha inputs, nf fields
     double *alpha;        // [j][stage][n]
-    unsigned short *awork;  // [j][stage][n]: bit 0 active, bits 1-2 harmonics, 3-4 exact-zero
-                            // harmonics, 5-15 Bessel terms
+    unsigned *awork;      // [j][stage][n]: the alpha's work counts; Albajar: bit 0 active,
+                          // bits 1-2 harmonics, 3-4 exact-zero harmonics, 5-15 Bessel terms;
+                          // warm: bits 0-6 larmornumber tests, 7-13 Faddeeva evaluations,
+                          // 14-20 warmdisp passes, 21-23 Larmor order
     double *psib;         // binned deposition: psi at the end of step k0 + j, [j][n]
     double *cbx;          // [c][6][n]: x, N at chunk boundary c (steps = c * chunk_steps)
     double *tx;           // [6][n]: the trajectory kernel's carry
@@ -890,6 +893,7 @@ struct SplitArgs {
     double *stau, *spsi, *sPdep;  // the scan's carry
     int *sinfo;           // steps | status << 24: the scan's stop
     int k0, kb;           // block: steps [k0, k0 + kb)
+    int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
 };
 
 __device__ __forceinline__ int info_steps(int v) { return v & 0xffffff; }
@@ -916,12 +920,19 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, const double *__re
         double Npar, inv;
         dispersion_grad(p, Nt, a.mode, k, &Npar, &inv);
         if constexpr (STORE) {
-            double *o = sp.ain + ((size_t)(j * 4 + st) * kAinF) * a.n + i;
+            double *o = sp.ain + ((size_t)(j * 4 + st) * sp.nf) * a.n + i;
+            const double N2 = Nt[0] * Nt[0] + Nt[1] * Nt[1] + Nt[2] * Nt[2];
             o[0] = p.X;
             o[(size_t)a.n] = p.Y;
-            o[2 * (size_t)a.n] = sqrt_pos(Nt[0] * Nt[0] + Nt[1] * Nt[1] + Nt[2] * Nt[2]);
             o[3 * (size_t)a.n] = Npar;
-            o[4 * (size_t)a.n] = exp_fast(p.lnTe);
+            if (sp.nf > kAinF) {  // the warm inputs as ray_rhs_m<2 / 3> forms them
+                o[2 * (size_t)a.n] = sqrt(N2);
+                o[4 * (size_t)a.n] = exp(p.lnTe);
+                o[kAinF * (size_t)a.n] = inv;
+            } else {
+                o[2 * (size_t)a.n] = sqrt_pos(N2);
+                o[4 * (size_t)a.n] = exp_fast(p.lnTe);
+            }
         }
         const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
         const double h = (st < 2) ? hds : a.ds;
@@ -1075,15 +1086,39 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     const int j = js >> 2;
     const int ti = sp.tinfo[i];
     if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
-    const double *in = sp.ain + (size_t)js * kAinF * a.n + i;
+    const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
     AlbajarWork work = {};
     const double al = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
         c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
         in[4 * (size_t)a.n], a.mode, &work);
     sp.alpha[(size_t)js * a.n + i] = al;
-    sp.awork[(size_t)js * a.n + i] =
-        (unsigned short)((work.n_active & 1u) | ((work.n_harm & 3u) << 1) | ((work.n_zero & 3u) << 3) |
-                         (min(work.n_terms, 2047u) << 5));
+    sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
+                                     ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5);
+}
+
+// the warm alpha (absorption 2 / 3, iwarm 1 / 3) at the stored stage points:
+// the same points and lanes as k_alpha_pts, with the group-velocity factor
+// stored by the trajectory kernel as the sixth input.  Without a ray's state
+// and step chain the heavy warm code has the registers to itself
+// (TORJ_WARM_ALPHA_WAVES waves per SIMD).
+#ifndef TORJ_WARM_ALPHA_WAVES
+#define TORJ_WARM_ALPHA_WAVES 1
+#endif
+template <int IWARM>
+__global__ void __launch_bounds__(256, TORJ_WARM_ALPHA_WAVES) k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
+    const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
+    const int i = q * 256 + threadIdx.x;
+    if (i >= a.n) return;
+    const int j = js >> 2;
+    const int ti = sp.tinfo[i];
+    if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
+    const double *in = sp.ain + (size_t)js * kAinFW * a.n + i;
+    const WarmAlpha r = alpha_warm_v<IWARM>(a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n],
+                                            in[3 * (size_t)a.n], in[4 * (size_t)a.n],
+                                            in[5 * (size_t)a.n], a.mode);
+    sp.alpha[(size_t)js * a.n + i] = r.alpha;
+    sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.ltrips, 127) | ((unsigned)min(r.nfad, 127) << 7) |
+                                     ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
 }
 
 // RK4 ray_segment from x, N over `k` steps without stores (the NaN-alpha replay)
@@ -1103,7 +1138,9 @@ __device__ void cold_replay(const TraceArgs &a, double x[3], double N[3], int k)
 template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
     const int i = blockIdx.x * 64 + threadIdx.x;
-    unsigned long long nsteps = 0, n_act = 0, n_harm = 0, n_terms = 0, n_zero = 0;
+    // counters [2..7] (include/torj_hip.h): Albajar or warm iwarm 1 meanings
+    unsigned long long nsteps = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
+    const int am = a.abs_model;
     if (i < a.n) {
         int steps = 0, st = ST_OK;
         double tau = 0.0, psi_a = 0.0, Pdep = 0.0;
@@ -1143,10 +1180,20 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const unsigned wk = sp.awork[o + q * (size_t)a.n];
-                    n_act += wk & 1u;
-                    n_harm += (wk >> 1) & 3u;
-                    n_zero += (wk >> 3) & 3u;
-                    n_terms += wk >> 5;
+                    if (am == 1) {
+                        c2 += wk & 1u;
+                        c3 += (wk >> 1) & 3u;
+                        c5 += (wk >> 3) & 3u;
+                        c4 += wk >> 5;
+                    } else if (am == 2) {
+                        const unsigned lrm = wk >> 21, passes = (wk >> 14) & 127u;
+                        c2 += wk & 127u;
+                        c3 += (wk >> 7) & 127u;
+                        c4 += passes;
+                        c5 += passes * lrm;
+                        c6 += lrm;
+                        c7 += lrm * lrm;
+                    }
                 }
                 const double Pn = exp(-taun);
                 const double dP = P - Pn;
@@ -1183,8 +1230,9 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
         }
     }
     if (a.counters) {
-        const unsigned long long s0 = wave_sum(nsteps), s2 = wave_sum(n_act), s3 = wave_sum(n_harm),
-                                 s4 = wave_sum(n_terms), s5 = wave_sum(n_zero);
+        const unsigned long long s0 = wave_sum(nsteps), s2 = wave_sum(c2), s3 = wave_sum(c3),
+                                 s4 = wave_sum(c4), s5 = wave_sum(c5), s6 = wave_sum(c6),
+                                 s7 = wave_sum(c7);
         if (threadIdx.x == 0) {
             atomicAdd(a.counters + 0, s0);
             atomicAdd(a.counters + 1, 4ull * s0);
@@ -1192,6 +1240,8 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
             atomicAdd(a.counters + 3, s3);
             atomicAdd(a.counters + 4, s4);
             atomicAdd(a.counters + 5, s5);
+            atomicAdd(a.counters + 6, s6);
+            atomicAdd(a.counters + 7, s7);
         }
     }
 }
@@ -2288,7 +2338,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         return (size_t)(e ? atol(e) : 1024) << 20;
     }();
     constexpr int R = torj_plasma_s::kRing;
-    const size_t per_step = 4 * kAinF * sizeof(double) * n;
+    const int nf = a.abs_model >= 2 ? kAinFW : kAinF;
+    const size_t per_step = 4 * (size_t)nf * sizeof(double) * n;
     long kb = (long)std::max<size_t>(1, budget / per_step);
     if (a.chunk_steps > 0 && kb >= a.chunk_steps) kb -= kb % a.chunk_steps;
     if (p->sched_mode == 3 && p->sched_waves > 0) kb = p->sched_waves;  // torj_set_sched(p, 3, steps per block)
@@ -2296,7 +2347,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int n_cb = (a.chunk_steps > 0 ? n_steps / a.chunk_steps : 0) + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t b_ain = al(per_step * kb), b_alpha = al(4 * sizeof(double) * n * kb),
-                 b_awork = al(4 * sizeof(unsigned short) * n * kb),
+                 b_awork = al(4 * sizeof(unsigned) * n * kb),
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
     const int nq = (int)((n + 255) / 256);
@@ -2313,7 +2364,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     for (int r = 0; r < R; r++) ain[r] = (double *)take(b_ain);
     SplitArgs sp{};
     sp.alpha = (double *)take(b_alpha);
-    sp.awork = (unsigned short *)take(b_awork);
+    sp.awork = (unsigned *)take(b_awork);
+    sp.nf = nf;
     double *psib[R] = {};
     if (b_psib)
         for (int r = 0; r < R; r++) psib[r] = (double *)take(b_psib);
@@ -2378,7 +2430,13 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
         HIPCK(hipEventRecord(p->ev_T[r], sT));
         HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
-        hipLaunchKernelGGL(k_alpha_pts, dim3((unsigned)(nq * 4 * sp.kb)), dim3(256), 0, s2, a, sp, nq);
+        const dim3 agrid((unsigned)(nq * 4 * sp.kb));
+        if (a.abs_model == 3)
+            hipLaunchKernelGGL(k_alpha_warm_pts<3>, agrid, dim3(256), 0, s2, a, sp, nq);
+        else if (a.abs_model == 2)
+            hipLaunchKernelGGL(k_alpha_warm_pts<1>, agrid, dim3(256), 0, s2, a, sp, nq);
+        else
+            hipLaunchKernelGGL(k_alpha_pts, agrid, dim3(256), 0, s2, a, sp, nq);
         TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s2, a, sp);
         HIPCK(hipEventRecord(p->ev_S[r], s2));
     }
@@ -2686,11 +2744,22 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
         const char *e = getenv("TORJ_SPLIT");
         return e ? atoi(e) : 1;
     }();
-    // the split RK4 path: fixed steps, Albajar (sched mode 3, or by default for
-    // beams that would use the work queue)
-    const bool use_split = !adaptive && cfg->absorption == 1 && cfg->n_steps > 0 &&
-                           (p->sched_mode == 3 ||
-                            (p->sched_mode < 0 && split_env == 1 && sched_env && G > p->n_cu * 4));
+    static const int split_warm_env = [] {  // -1 auto, 0 off, 1 on
+        const char *e = getenv("TORJ_SPLIT_WARM");
+        return e ? atoi(e) : -1;
+    }();
+    // the split RK4 path (fixed steps; sched mode 3 forces it):
+    //  * Albajar: by default for beams that would use the work queue;
+    //  * warm (2, 3): by default for beams of fewer 64-ray groups than 3 per CU,
+    //    where the one-wave-per-SIMD warm queue kernel leaves SIMDs idle and the
+    //    split's alpha kernel spreads the points over all of them (129 rays,
+    //    model 3: 13.1 s -> 0.1 s); on the 1e5-ray fan the queue kernel is faster
+    //    (C5 221 vs 234 ms, model 3 19.7 vs 20.6 s)
+    const bool albajar_split = cfg->absorption == 1 && split_env == 1 && sched_env && G > p->n_cu * 4;
+    const bool warm_split = cfg->absorption >= 2 && split_env == 1 &&
+                            (split_warm_env == 1 || (split_warm_env < 0 && G < p->n_cu * 3));
+    const bool use_split = !adaptive && cfg->absorption >= 1 && cfg->n_steps > 0 &&
+                           (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
     if (use_split) {
         if (split_trace(p, a, DM, tr, cs, s)) return -1;
     } else if (use_sched && cfg->n_steps > 0) {
