@@ -224,12 +224,16 @@ def main():
         at = ABSORPTION[args.absorption]  # ABS template: 0 cold, 1 Albajar, 2 / 3 warm iwarm 1 / 3
         # the library's default for a large fixed-step Albajar beam: the split
         # pipeline -- its kernels are timed together as the trace phase
-        split = (sched and not adaptive and args.absorption == "albajar"
-                 and os.environ.get("TORJ_SPLIT", "1") == "1")
+        sw = os.environ.get("TORJ_SPLIT_WARM", "-1")
+        split = (not adaptive and os.environ.get("TORJ_SPLIT", "1") == "1"
+                 and ((sched and args.absorption == "albajar")
+                      or (args.absorption == "warm_wr" and sw != "0")
+                      or (args.absorption == "warm_fr" and (sw == "1" or (sw != "0" and (n + 63) // 64 < 3 * n_simd // 4)))))
         # small Albajar beams run 16 lanes per ray (the library's automatic choice)
         lpr16 = (not sched and at == 1 and dm == 2 and os.environ.get("TORJ_LPR", "0") != "1"
                  and n * 16 <= n_simd * 2 * 64)
-        kname = (SPLIT_KERNELS if split
+        kname = ((SPLIT_KERNELS if at == 1 else SPLIT_KERNELS.replace("k_alpha_pts", "k_alpha_warm_pts"))
+                 if split
                  else f"k_trace_sched<{at}, {dm}, true, {int(adaptive)}>" if sched
                  else f"k_trace<{at}, {dm}, true, 16>" if lpr16
                  else f"k_trace<{at}, {dm}, true>")  # rocprof's name of the instance

@@ -261,8 +261,9 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
  * warm absorption): the trajectories' cold RK4 in one kernel, the 4 x n_steps
  * alpha evaluations per ray in a fully parallel one, the optical depth by an
  * in-order scan, blocks of steps pipelined over two streams (DESIGN.md 3.7;
- * mode -1 picks it for Albajar where it would pick 1, and for the warm models
- * on beams of fewer than 3 x 64-ray groups per CU, unless env TORJ_SPLIT=0;
+ * mode -1 picks it for Albajar where it would pick 1, for the weakly
+ * relativistic warm model always and for the fully relativistic one on beams
+ * of fewer than 3 x 64-ray groups per CU, unless env TORJ_SPLIT=0;
  * TORJ_SPLIT_WARM=0 / 1 turns the warm choice off / on for every size).
  * waves: number of persistent waves for mode 1 (0 = default: min(8 per CU, G - G/16));
  * steps per pipeline block for mode 3 (0 = from the 1 GiB per alpha-input

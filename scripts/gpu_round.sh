@@ -13,7 +13,7 @@ bash scripts/profile.sh prof_c3 || exit 1
 python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles "k_traj|k_alpha_pts|k_tau_scan|k_split_final" || exit 1
 python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_fit_depo depo_ || exit 1
 bash scripts/profile.sh prof_c5 --absorption warm_wr || exit 1
-python tools/prof_summary.py gpurun_out/prof_c5 $O/profiles k_trace c5_ || exit 1
+python tools/prof_summary.py gpurun_out/prof_c5 $O/profiles "k_traj|k_alpha_warm_pts|k_tau_scan|k_split_final" c5_ || exit 1
 mkdir -p profiles/$R && cp $O/profiles/*.json $O/profiles/*.csv profiles/$R/ 2>/dev/null
 timeout -k 10 600 python bench.py > $O/bench_c3.log 2>&1 || { tail -20 $O/bench_c3.log; exit 1; }
 grep '^{' $O/bench_c3.log

@@ -1100,12 +1100,17 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
 // the same points and lanes as k_alpha_pts, with the group-velocity factor
 // stored by the trajectory kernel as the sixth input.  Without a ray's state
 // and step chain the heavy warm code has the registers to itself
-// (TORJ_WARM_ALPHA_WAVES waves per SIMD).
-#ifndef TORJ_WARM_ALPHA_WAVES
-#define TORJ_WARM_ALPHA_WAVES 1
+// (waves per SIMD: iwarm 1 two -- 221 ms fused, 235 at one wave, 166 at two on
+// the C5 beam; iwarm 3 one -- 20.4 s, 22.2 s at two).
+#ifndef TORJ_WARM1_ALPHA_WAVES
+#define TORJ_WARM1_ALPHA_WAVES 2
+#endif
+#ifndef TORJ_WARM3_ALPHA_WAVES
+#define TORJ_WARM3_ALPHA_WAVES 1
 #endif
 template <int IWARM>
-__global__ void __launch_bounds__(256, TORJ_WARM_ALPHA_WAVES) k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
+__global__ void __launch_bounds__(256, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
+    k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
     const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
     const int i = q * 256 + threadIdx.x;
     if (i >= a.n) return;
@@ -2750,14 +2755,17 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     }();
     // the split RK4 path (fixed steps; sched mode 3 forces it):
     //  * Albajar: by default for beams that would use the work queue;
-    //  * warm (2, 3): by default for beams of fewer 64-ray groups than 3 per CU,
-    //    where the one-wave-per-SIMD warm queue kernel leaves SIMDs idle and the
-    //    split's alpha kernel spreads the points over all of them (129 rays,
-    //    model 3: 13.1 s -> 0.1 s); on the 1e5-ray fan the queue kernel is faster
-    //    (C5 221 vs 234 ms, model 3 19.7 vs 20.6 s)
+    //  * warm weakly relativistic (2): by default -- its alpha kernel runs two
+    //    waves per SIMD where the fused queue kernel holds one (C5: 165 vs 221 ms);
+    //  * warm fully relativistic (3): by default for beams of fewer 64-ray groups
+    //    than 3 per CU, where the one-wave-per-SIMD queue kernel leaves SIMDs idle
+    //    and the split's alpha kernel spreads the points over all of them (129
+    //    rays: 13.1 s -> 0.1 s); on the 1e5-ray fan the queue kernel is faster
+    //    (19.7 vs 20.4 s)
     const bool albajar_split = cfg->absorption == 1 && split_env == 1 && sched_env && G > p->n_cu * 4;
     const bool warm_split = cfg->absorption >= 2 && split_env == 1 &&
-                            (split_warm_env == 1 || (split_warm_env < 0 && G < p->n_cu * 3));
+                            (split_warm_env == 1 ||
+                             (split_warm_env < 0 && (cfg->absorption == 2 || G < p->n_cu * 3)));
     const bool use_split = !adaptive && cfg->absorption >= 1 && cfg->n_steps > 0 &&
                            (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
     if (use_split) {
