@@ -1652,9 +1652,10 @@ struct torj_plasma_s {
     // alpha / scan kernels and the pipeline's events
     void *d_split = nullptr;
     size_t split_cap = 0;
-    hipStream_t stream2 = nullptr, streamT = nullptr;  // alpha + scan; trajectory (high priority)
+    hipStream_t stream2 = nullptr, streamT = nullptr;  // alpha; trajectory (high priority)
+    hipStream_t streamS = nullptr;                      // optical-depth scan
     static constexpr int kRing = 4;                     // alpha-input buffers in flight
-    hipEvent_t ev_T[kRing] = {}, ev_S[kRing] = {}, ev_J = nullptr, ev_F = nullptr;
+    hipEvent_t ev_T[kRing] = {}, ev_A[kRing] = {}, ev_S[kRing] = {}, ev_J = nullptr, ev_F = nullptr;
 };
 
 static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
@@ -1744,8 +1745,10 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
         HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
+        HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
+            HIPCK(hipEventCreateWithFlags(&p->ev_A[q], hipEventDisableTiming));
             HIPCK(hipEventCreateWithFlags(&p->ev_S[q], hipEventDisableTiming));
         }
         HIPCK(hipEventCreateWithFlags(&p->ev_J, hipEventDisableTiming));
@@ -1987,12 +1990,14 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->d_batch) (void)hipFree(p->d_batch);
     for (int q = 0; q < torj_plasma_s::kRing; q++) {
         if (p->ev_T[q]) (void)hipEventDestroy(p->ev_T[q]);
+        if (p->ev_A[q]) (void)hipEventDestroy(p->ev_A[q]);
         if (p->ev_S[q]) (void)hipEventDestroy(p->ev_S[q]);
     }
     if (p->ev_J) (void)hipEventDestroy(p->ev_J);
     if (p->ev_F) (void)hipEventDestroy(p->ev_F);
     if (p->stream2) (void)hipStreamDestroy(p->stream2);
     if (p->streamT) (void)hipStreamDestroy(p->streamT);
+    if (p->streamS) (void)hipStreamDestroy(p->streamS);
     delete p;
     return 0;
 }
@@ -2356,7 +2361,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
     const int nq = (int)((n + 255) / 256);
-    const size_t bytes = R * b_ain + b_alpha + b_awork + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
+    const size_t bytes = R * (b_ain + b_alpha + b_awork) + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
                          2 * b_n4;
     if (ensure_split(p, bytes)) return -1;
     char *q = (char *)p->d_split;
@@ -2368,8 +2373,12 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     double *ain[R];
     for (int r = 0; r < R; r++) ain[r] = (double *)take(b_ain);
     SplitArgs sp{};
-    sp.alpha = (double *)take(b_alpha);
-    sp.awork = (unsigned *)take(b_awork);
+    double *alphas[R];
+    unsigned *aworks[R];
+    for (int r = 0; r < R; r++) {
+        alphas[r] = (double *)take(b_alpha);
+        aworks[r] = (unsigned *)take(b_awork);
+    }
     sp.nf = nf;
     double *psib[R] = {};
     if (b_psib)
@@ -2386,11 +2395,20 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const char *e = getenv("TORJ_SPLIT_SERIAL");
         return e && atoi(e) != 0;
     }();
+    // the scan on a third stream (TORJ_SPLIT_SCAN=0: behind the alpha kernel on
+    // the second), so the alpha kernel of block b + 1 need not wait for the
+    // latency-bound one-lane-per-ray scan of block b
+    static const bool scan_own = [] {
+        const char *e = getenv("TORJ_SPLIT_SCAN");
+        return !e || atoi(e) != 0;
+    }();
     hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
+    hipStream_t s3 = serial ? s : (scan_own ? p->streamS : p->stream2);
     if (!serial) {  // fork from the caller's stream
         HIPCK(hipEventRecord(p->ev_F, s));
         HIPCK(hipStreamWaitEvent(sT, p->ev_F, 0));
         HIPCK(hipStreamWaitEvent(s2, p->ev_F, 0));
+        if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_F, 0));
     }
     // the scan's carry starts at (steps 0, OK), tau = 0, P_dep = 0
     HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, sT));
@@ -2427,7 +2445,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const int r = b % R;
         sp.ain = ain[r];
         sp.psib = psib[r];
-        // this buffer's previous reader (alpha and scan of block b - R) is done
+        sp.alpha = alphas[r];
+        sp.awork = aworks[r];
+        // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
         if (lds_traj)
             TORJ_SPLIT_DISPATCH(k_traj_lds, dim3(nblocks(G, wpb)), dim3(64 * wpb), lds_bytes, sT, a, sp);
@@ -2442,13 +2462,16 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             hipLaunchKernelGGL(k_alpha_warm_pts<1>, agrid, dim3(256), 0, s2, a, sp, nq);
         else
             hipLaunchKernelGGL(k_alpha_pts, agrid, dim3(256), 0, s2, a, sp, nq);
-        TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s2, a, sp);
-        HIPCK(hipEventRecord(p->ev_S[r], s2));
+        HIPCK(hipEventRecord(p->ev_A[r], s2));
+        if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_A[r], 0));
+        TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s3, a, sp);
+        HIPCK(hipEventRecord(p->ev_S[r], s3));
     }
-    TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s2, a, sp);
+    TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
 #undef TORJ_SPLIT_DISPATCH
-    if (!serial) {  // join: the final kernel followed every scan, and each scan its trajectory
-        HIPCK(hipEventRecord(p->ev_J, s2));
+    if (!serial) {  // join: the final kernel followed every scan, each scan its alpha kernel
+                    // and each alpha kernel its trajectory
+        HIPCK(hipEventRecord(p->ev_J, s3));
         HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
     }
     HIPCK(hipGetLastError());
