@@ -9,6 +9,7 @@ O=gpurun_out/round
 mkdir -p $O/profiles
 timeout -k 10 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
+timeout -k 10 300 python scripts/alpha_sweep_stats.py > $O/profiles/alpha_sweep.json 2> $O/alpha_sweep.err || { tail -20 $O/alpha_sweep.err; exit 1; }
 bash scripts/profile.sh prof_c3 || exit 1
 python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles "k_traj|k_alpha_pts|k_tau_scan|k_split_final" || exit 1
 python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_fit_depo depo_ || exit 1

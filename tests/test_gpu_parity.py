@@ -99,6 +99,40 @@ def test_albajar_golden_sweep(gpu, T):
         assert np.abs(a[ok & ~big] - want[ok & ~big]).max() < 1e-20
 
 
+def albajar_random_sweep(T, O, n=20000, seed=7):
+    """GPU vs oracle abs_Albajar_fast on n random physical tuples (both modes,
+    harmonics 2 and 3 resonant or not, Te 50 eV - 20 keV).  Returns the relative
+    errors where |alpha| > 1e-12 /m and the absolute errors elsewhere."""
+    rng = np.random.default_rng(seed)
+    om = 2 * np.pi * 92.5e9
+    X = rng.uniform(0.02, 0.98, n)
+    Y = rng.uniform(0.3, 0.75, n)
+    N_abs = rng.uniform(0.3, 1.0, n)
+    N_par = N_abs * rng.uniform(-0.9, 0.9, n)
+    Te = np.exp(rng.uniform(np.log(50.0), np.log(2e4), n))
+    mode = np.where(rng.random(n) < 0.5, -1, 1)
+    a = np.empty(n)
+    for m in (-1, 1):
+        s = mode == m
+        a[s] = T.abs_Albajar_fast(om, X[s], Y[s], N_abs[s], N_par[s], Te[s], m)
+    want = np.array([O.abs_albajar_fast(om, X[i], Y[i], N_abs[i], N_par[i], Te[i], int(mode[i]))
+                     for i in range(n)])
+    assert np.array_equal(np.isnan(a), np.isnan(want))
+    ok = ~np.isnan(want)
+    big = ok & (np.abs(want) > 1e-12)
+    inputs = np.stack([X, Y, N_abs, N_par, Te, mode, a, want], 1)
+    return rel_err(a[big], want[big]), np.abs(a[ok & ~big] - want[ok & ~big]), inputs[big]
+
+
+def test_albajar_random_physical_sweep(gpu, T, O):
+    """The node loop's exp_node / sqrt_node (torj_math.hpp) keep alpha within the
+    1e-10 parity bar of the libm oracle on 20 000 random physical inputs."""
+    rel, ab, _ = albajar_random_sweep(T, O)
+    assert len(rel) > 5000  # most tuples absorb
+    assert rel.max() < 1e-10
+    assert ab.max() < 1e-20
+
+
 def test_albajar_matches_oracle_along_rays(gpu, T, hplasma, oplasma, fan_states):
     for mode in (1, -1):
         xp, Np, w, om = fan_states[mode]

@@ -1,4 +1,5 @@
-"""Coefficients of the node-loop exp polynomial (torj_math.hpp exp_nonpos).
+"""Coefficients of the device exp polynomials (torj_math.hpp exp_fast: degree
+11; exp_node, the Albajar node loop: degree 9 -- `python tools/gen_exp_poly.py 9`).
 
 e^r on |r| <= ln2/2 as 1 + r + r^2 q(r), q of degree 9 interpolated at its
 Chebyshev nodes in 50-digit arithmetic (near-minimax): degree 11 overall, max
@@ -32,7 +33,8 @@ def max_ulp(co):
 
 
 if __name__ == "__main__":
-    co = fit(11)
+    import sys
+    co = fit(int(sys.argv[1]) if len(sys.argv) > 1 else 11)
     print("max error %.2f ulp" % max_ulp(co))
     for k, v in enumerate(co):
         print(f"c{k} = {v!r}")

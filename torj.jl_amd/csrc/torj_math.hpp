@@ -80,10 +80,10 @@ TORJ_HD double rcp_nz(double x) {
     return fma(r, e, r);
 }
 
-// sqrt of a finite positive normal argument (lengths, |B|, |dD/dN|, the
-// node-loop gamma): on the device v_rsq_f64 + one Goldschmidt step + one Newton
-// correction (~1 ulp; the library sequence adds a second correction for correct
-// rounding plus denormal scaling and class checks).
+// sqrt of a finite positive normal argument (lengths, |B|, |dD/dN|): on the
+// device v_rsq_f64 + one Goldschmidt step + one Newton correction (~1 ulp; the
+// library sequence adds a second correction for correct rounding plus denormal
+// scaling and class checks).
 TORJ_HD double sqrt_pos(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double y = __builtin_amdgcn_rsq(x);
@@ -97,10 +97,26 @@ TORJ_HD double sqrt_pos(double x) {
 #endif
 }
 
+// gamma of the Albajar node loop: v_rsq_f64 + the Goldschmidt step of sqrt_pos
+// without its Newton correction (a few ulp).  gamma enters only as
+// exp(mu (1 - gamma)) with mu (gamma - 1) < 760 on every node that is not an
+// exact zero, so a relative error e moves a node term by ~mu gamma e; the
+// Albajar golden sweep and the headline-fan parity hold at 1e-10 (C3 trace
+// phase -2.5 % on top of exp_node).
+TORJ_HD double sqrt_node(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(x);
+    const double g = x * y, h = 0.5 * y;
+    return fma(g, fma(-h, g, 0.5), g);
+#else
+    return sqrt(x);
+#endif
+}
+
 // exp on the device: range reduction + degree-11 near-minimax polynomial +
 // ldexp (~1 ulp).  No special-case paths: ldexp overflows to inf above ~709
-// and underflows to 0 below ~-745, NaN stays NaN.  Used for the node loop's
-// exp(mu (1 - gamma)) and for n_e, T_e from their log splines.
+// and underflows to 0 below ~-745, NaN stays NaN.  Used for n_e, T_e from
+// their log splines (the node loop takes exp_node below).
 TORJ_HD double exp_fast(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double k = __builtin_rint(x * 1.4426950408889634074);
@@ -122,6 +138,35 @@ TORJ_HD double exp_fast(double x) {
     p = fma(p, r, 1.0);
     // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
     // and ldexp of a huge negative exponent underflows to 0
+    int ki;
+    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
+    return __builtin_amdgcn_ldexp(p, ki);
+#else
+    return exp(x);
+#endif
+}
+
+// exp of the Albajar node loop, exp(mu (1 - gamma)): the same range reduction
+// with a degree-9 near-minimax polynomial (tools/gen_exp_poly.py 9: 333 ulp,
+// 7.4e-14 relative).  Each node term carries it once; the harmonic sum stays
+// within ~1e-13 of the libm one, three orders under the 1e-10 parity bar, and
+// the two fma saved per exp are 4 of the pair's ~100 VALU instructions
+// (C3 trace phase -1.8 %).
+TORJ_HD double exp_node(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double k = __builtin_rint(x * 1.4426950408889634074);
+    double r = fma(-k, 6.93147180559945286227e-01, x);
+    r = fma(-k, 2.31904681384629955842e-17, r);
+    double p = 2.7617564785876086e-06;
+    p = fma(p, r, 2.4867870179687727e-05);
+    p = fma(p, r, 0.00019841224599656011);
+    p = fma(p, r, 0.0013888839110572009);
+    p = fma(p, r, 0.00833333334420298);
+    p = fma(p, r, 0.04166666678626573);
+    p = fma(p, r, 0.16666666666662586);
+    p = fma(p, r, 0.4999999999995511);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
     int ki;
     asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
     return __builtin_amdgcn_ldexp(p, ki);
@@ -562,11 +607,11 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double P = fma(A, fma(c.K3, t2, c.K0), fma(Cc, c.K1, -B));
     const double wp = w * p;
     const double a = fma(c.C1, t2, c.C0);
-    if (single) return wp * P * exp_fast(fma(-c.mu, sqrt_pos(a), c.mu));
+    if (single) return wp * P * exp_node(fma(-c.mu, sqrt_node(a), c.mu));
     const double Q = fma(A, c.K4, Cc * c.K5);
     const double b = c.C2 * t;
-    const double Ep = exp_fast(fma(-c.mu, sqrt_pos(a + b), c.mu));
-    const double Em = exp_fast(fma(-c.mu, sqrt_pos(a - b), c.mu));
+    const double Ep = exp_node(fma(-c.mu, sqrt_node(a + b), c.mu));
+    const double Em = exp_node(fma(-c.mu, sqrt_node(a - b), c.mu));
     return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 
