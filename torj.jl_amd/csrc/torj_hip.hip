@@ -882,7 +882,7 @@ constexpr int kAinFW = 6;
 struct SplitArgs {
     double *ain;          // [j][stage][f][n]: this block's alpha inputs, nf fields
     double *alpha;        // [j][stage][n]
-    unsigned *awork;      // [j][stage][n]: the alpha's work counts; Albajar: bit 0 active,
+    unsigned *awork;      // [j][stage][n] (null unless counted): alpha work counts; Albajar: bit 0 active,
                           // bits 1-2 harmonics, 3-4 exact-zero harmonics, 5-15 Bessel terms;
                           // warm: bits 0-6 larmornumber tests, 7-13 Faddeeva evaluations,
                           // 14-20 warmdisp passes, 21-23 Larmor order
@@ -1090,9 +1090,10 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     AlbajarWork work = {};
     const double al = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
         c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
-        in[4 * (size_t)a.n], a.mode, &work);
+        in[4 * (size_t)a.n], a.mode, sp.awork ? &work : nullptr);
     sp.alpha[(size_t)js * a.n + i] = al;
-    sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
+    if (sp.awork)  // a counted launch (null otherwise: no work words written or read)
+        sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5);
 }
 
@@ -1122,7 +1123,8 @@ __global__ void __launch_bounds__(256, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TOR
                                             in[3 * (size_t)a.n], in[4 * (size_t)a.n],
                                             in[5 * (size_t)a.n], a.mode);
     sp.alpha[(size_t)js * a.n + i] = r.alpha;
-    sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.ltrips, 127) | ((unsigned)min(r.nfad, 127) << 7) |
+    if (sp.awork)
+        sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.ltrips, 127) | ((unsigned)min(r.nfad, 127) << 7) |
                                      ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
 }
 
@@ -1183,7 +1185,7 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
                     break;
                 }
 #pragma unroll
-                for (int q = 0; q < 4; q++) {
+                for (int q = 0; q < 4 && sp.awork; q++) {
                     const unsigned wk = sp.awork[o + q * (size_t)a.n];
                     if (am == 1) {
                         c2 += wk & 1u;
@@ -2446,7 +2448,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.ain = ain[r];
         sp.psib = psib[r];
         sp.alpha = alphas[r];
-        sp.awork = aworks[r];
+        sp.awork = a.counters ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
         if (lds_traj)
