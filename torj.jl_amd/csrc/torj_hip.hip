@@ -1028,7 +1028,7 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
         double psi_b = 0.0;
         if (DEPO != kDepoNone || check)
-            psi_b = eval_one<NS>(coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
+            psi_b = eval_one<NS>(coef, a.g, sqrt_pos(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
         if constexpr (DEPO == kDepoSamples) a.smp_psi[smp_at(steps, i, a.smp_rows)] = psi_b;
         if constexpr (DEPO == kDepoBinned) sp.psib[(size_t)(s - sp.k0) * a.n + i] = psi_b;
         if constexpr (TRAJ) {

@@ -335,7 +335,7 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
     const double Np2 = Npar * Npar, Y2 = Y * Y, invY = rcp_nz(Y), invY2 = invY * invY;
     const double om = 1.0 - Np2, omX = 1.0 - X;
     const double Delta = om * om + 4.0 * Np2 * omX * invY2;
-    const double sq = sqrt(Delta);
+    const double sq = sqrt_nn(Delta);
     const double A = 1.0 + md * sq + Np2;
     const double Q = 2.0 * (-1.0 + X + Y2);
     const double invQ = rcp_nz(Q);
@@ -610,9 +610,15 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     double Sm, Sm1;
     sc.eval(-h2, Sm, Sm1);
     const double Sl = fma(-h2, Sm1, md * Sm);  // S_{m-1} by the downward recurrence
-    double p = h;  // h^(2m-1)
+    double p = h;  // h^(2m-1): h^3 = h^2 h, h^5 = (h^2 h^2) h
+    if constexpr (M == 2) {
+        p = h2 * h;
+    } else if constexpr (M == 3) {
+        p = (h2 * h2) * h;
+    } else {
 #pragma unroll
-    for (int k = 1; k < 2 * M - 1; k++) p *= h;
+        for (int k = 1; k < 2 * M - 1; k++) p *= h;
+    }
     const double hSm = h * Sm;
     const double A = hSm * Sm;
     const double T1 = h2 * Sm1;
@@ -777,7 +783,8 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
 #ifdef __HIP_DEVICE_COMPILE__
     level = __ballot(level == 4) ? 4 : (__ballot(level == 3) ? 3 : (__ballot(level == 2) ? 2 : (__ballot(level == 1) ? 1 : 0)));
 #endif
-    const double Pm = md / (N_perp * omega_bar);
+    const double den = N_perp * omega_bar;
+    const double Pm = den == 0.0 ? INFINITY : md * rcp_nz(den);
     if (zero) {
         if (work) work->n_zero++;
         return -mu * Pm * Pm * 0.0 * sq_r;
@@ -795,8 +802,8 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
         case 3: sum = node_sum<M, 3, LPR, U>(gl, c, sub); break;
         default: sum = node_sum<M, 4, LPR, U>(gl, c, sub); break;
     }
-    // (m / (N_perp omega_bar))^2: IEEE quotient, N_perp = 0 (parallel
-    // propagation) stays an infinity as in the reference
+    // (m / (N_perp omega_bar))^2 with Pm from a reciprocal (<= 1 ulp); N_perp = 0
+    // (parallel propagation) stays an infinity as in the reference's quotient
     return -mu * Pm * Pm * sum * sq_r;
 }
 
