@@ -77,6 +77,14 @@ def parse():
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE = {world}: launch one process per GPU "
+                 f"with --nproc-per-node equal to --gpus")
+    if world == 1 and args.gpus > 1:
+        return main_library(args)  # one process, N devices: make_beam's library path
+    if args.gpus < 1:
+        sys.exit(f"bench.py: --gpus {args.gpus} < 1")
     import torch
     import torch.distributed as dist
 
@@ -85,7 +93,6 @@ def main():
     from torj_hip import synthetic as S
     from torj_hip.parallel import allreduce_deposition
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
@@ -337,6 +344,191 @@ def main():
         dist.destroy_process_group()
 
 
+def main_library(args):
+    """`python bench.py --gpus N` in ONE process (no torchrun): make_beam's
+    library path over N devices, torj_trace_beam_device -- device-resident ray
+    shards (inputs in HBM before the timed region), one host thread + stream per
+    device, then the RCCL all-reduce of the (n_psi + 1) deposition vector
+    (src/solve.jl:209-240).  Weak scaling (default): each device its own beam,
+    rotated toroidally by 2 pi k / N; --shard: ONE fan cut into N contiguous
+    64-ray-aligned shards (C4, strong).  Exits non-zero before any GPU work when
+    fewer than N devices are visible.  TORJ_BEAM_SAME_DEVICE=1 rehearses the
+    N-replica path on device 0 (labelled in the line; not a scaling figure)."""
+    import ctypes
+
+    import torch
+
+    same = os.environ.get("TORJ_BEAM_SAME_DEVICE", "0") not in ("", "0")
+    n_vis = torch.cuda.device_count()  # does not initialise the GPU on this image
+    if n_vis < args.gpus and not same:
+        print(f"bench.py: --gpus {args.gpus} needs {args.gpus} visible HIP devices, found {n_vis}",
+              file=sys.stderr, flush=True)
+        sys.exit(2)
+    torch.cuda.init()  # torch's HIP runtime first, then the library's (tests/conftest.py)
+    import torj_hip as T
+    from torj_hip import flops as F
+    from torj_hip import synthetic as S
+    from torj_hip.parallel import group_shard, trace_beam_device
+
+    N = args.gpus
+    eq = S.circular_tokamak()
+    plasma = T.Plasma(*S.plasma_args(eq), device=0)
+    T.abs_Al_init(24)
+    f = args.freq
+    omega = 2 * np.pi * f
+    setup = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(setup["steering_angle_pol"], setup["steering_angle_tor"])
+    x0 = np.array([setup["R0"], 0.0, setup["z0"]])
+    pos, dirs, w = T.launch_peripheral_rays(x0, N0, setup["spot_size"], setup["inverse_curvature_radius"],
+                                            f, N_rings=args.n_rings, min_azimuthal_points=args.min_az)
+    n_fan = len(w)
+    parts = []  # per device: (launch points, directions, weights)
+    for k in range(N):
+        if args.shard:
+            sl = group_shard(n_fan, N, k)
+            parts.append((pos[sl], dirs[sl], w[sl]))
+        else:
+            phi = 2 * np.pi * k / N
+            rot = np.array([[np.cos(phi), -np.sin(phi), 0], [np.sin(phi), np.cos(phi), 0], [0, 0, 1]])
+            parts.append((pos @ rot.T, dirs @ rot.T, w))
+    grid = np.linspace(0.0, 1.0, args.n_psi)
+    adaptive = args.integrator == "adaptive"
+    cap = 2 * args.n_steps + 400 if adaptive else args.n_steps
+    n_save = cap // args.traj_stride if args.traj_stride > 0 else 0
+    dep = 1 if args.deposition == "reference" else 0
+    cfg = T._lib.TraceCfg(omega, args.mode, args.ds, cap, max(1, args.n_steps // 100), 1.0, 1e-6,
+                          ABSORPTION[args.absorption], args.traj_stride, dep, int(adaptive), 1e-6,
+                          1e-6, args.n_steps * args.ds, 100)
+    shards = []
+    for k, (p_k, d_k, w_k) in enumerate(parts):
+        xp, Np, s0, st = T.ray_entry(plasma, p_k, d_k, omega, args.mode, gpu=True)
+        if not (st == 0).all():
+            raise RuntimeError(f"ray entry failed for {(st != 0).sum()} rays of shard {k}")
+        dev = torch.device("cuda", 0 if same else k % n_vis)
+        n = len(w_k)
+
+        def d(a, dtype=torch.float64):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dtype)
+
+        shards.append(dict(
+            n=n, x0=d(xp.T), N0=d(Np.T), weights=d(w_k), psi_grid=d(grid), x_launch=d(p_k.T), s0=d(s0),
+            state=torch.empty((7, n), dtype=torch.float64, device=dev),
+            status=torch.empty(n, dtype=torch.int32, device=dev),
+            steps=torch.empty(n, dtype=torch.int32, device=dev),
+            dP_shell=torch.zeros(args.n_psi + 1, dtype=torch.float64, device=dev),
+            P_dep=torch.empty(n, dtype=torch.float64, device=dev),
+            traj=(torch.empty((n_save, 5, n), dtype=torch.float64, device=dev) if n_save else None),
+            counters=torch.zeros(8, dtype=torch.int64, device=dev)))
+    devs = sorted({sh["state"].device.index for sh in shards})
+
+    def sync():
+        for i in devs:
+            torch.cuda.synchronize(i)
+
+    def step(counted=False):
+        for sh in shards:  # make_beam's sums start at 0 (the trace accumulates)
+            sh["dP_shell"].zero_()
+        sync()  # torch's zeroing before the library's own streams read them
+        trace_beam_device(plasma, cfg, args.n_psi,
+                          [dict(sh, counters=sh["counters"] if counted else None) for sh in shards])
+
+    def progress(msg):
+        print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+    step(counted=True)
+    cnt = [sh["counters"].cpu().numpy().astype(np.int64) for sh in shards]
+    ray_steps = int(sum(c[0] for c in cnt))
+    progress("counted launch done")
+    for k in range(args.warmup):
+        step()
+        progress(f"warmup {k + 1}/{args.warmup} done")
+    sync()
+    L = T.lib()
+    T._lib.check(L.torj_timing(plasma.handle, 1))  # replica 0 is the handle: device 0's phases
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    sync()
+    elapsed = time.perf_counter() - t0
+    progress(f"timed region done: {elapsed:.2f} s")
+    n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+    T._lib.check(L.torj_timing_read(plasma.handle, ctypes.byref(n_calls), ctypes.byref(t_trace),
+                                    ctypes.byref(t_post)))
+    T._lib.check(L.torj_timing(plasma.handle, 0))
+    kern_ms = t_trace.value / max(n_calls.value, 1)
+    post_ms = t_post.value / max(n_calls.value, 1)
+    # the fan-out + reduce overhead alone: empty shards, the same deposition vectors
+    empty = [dict(n=0, psi_grid=sh["psi_grid"], dP_shell=sh["dP_shell"]) for sh in shards]
+    t1 = time.perf_counter()
+    for _ in range(20):
+        trace_beam_device(plasma, cfg, args.n_psi, empty)
+    reduce_ms = (time.perf_counter() - t1) / 20 * 1e3
+    ms_per_step = elapsed / args.steps * 1e3
+    value = ray_steps / (ms_per_step / 1e3)
+    flop0 = (F.algorithmic_flops(cnt[0], n_gl=24) if args.absorption in ("albajar", "none")
+             else F.algorithmic_flops_warm(cnt[0]) if args.absorption == "warm_wr" else None)
+    achieved = flop0 / (kern_ms / 1e3) / 1e12 if flop0 is not None and kern_ms > 0 else None
+    dP0 = shards[0]["dP_shell"].cpu().numpy()
+    agree = max(float(np.abs(sh["dP_shell"].cpu().numpy() - dP0).max()) for sh in shards)
+    placement = ("same-device rehearsal (TORJ_BEAM_SAME_DEVICE=1): all replicas on device 0, partials "
+                 "summed on the host -- not a scaling measurement" if same else
+                 f"replica k on device k (of {n_vis} visible), RCCL all-reduce over xGMI")
+    out = {
+        "metric": "ray-steps/sec, 1e5-ray EC fan on 1 MI355X (+ 2/4/8-GPU scaling)",
+        "value": value,
+        "unit": "ray-steps/s",
+        "n_gpus": N,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong" if args.shard else "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic circular-tokamak equilibrium (analytic, sampled on 56x56) + "
+                "launch_peripheral_rays fan",
+        "config": {
+            "workload": (f"{'C4' if args.shard else 'C3'} via the library path torj_trace_beam_device: "
+                         + (f"{n_fan}-ray EC fan sharded over {N} devices" if args.shard
+                            else f"{n_fan}-ray EC fan per device") +
+                         f" (N_rings={args.n_rings}, min_az={args.min_az}), X-mode {f/1e9:.1f} GHz, "
+                         f"{args.n_steps} RK4 steps ds={args.ds:g} m ({args.integrator}), "
+                         f"{ALPHA_NAME[args.absorption]}, psi-shell deposition n_psi={args.n_psi} "
+                         f"({args.deposition}), traj stride {args.traj_stride}"),
+            "rays_per_device": [sh["n"] for sh in shards],
+            "rays_total": int(sum(sh["n"] for sh in shards)),
+            "rk4_steps": args.n_steps,
+            "n_psi": args.n_psi,
+            "absorption": args.absorption,
+            "parallelism": (f"one process, {N} replicas (host thread + stream each), device-resident "
+                            f"ray shards, RCCL all-reduce of dP_shell"),
+            "placement": placement,
+            "n_devices_used": len(devs),
+        },
+        "roofline": {
+            "bound": "fp64-valu",
+            "achieved": achieved,
+            "peak": FP64_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / FP64_VECTOR_PEAK_TFLOPS if achieved is not None else None,
+            "traffic": None,
+            "note": "device 0's trace phase (library HIP events) and its shard's counted FLOPs",
+            "kernel_ms": kern_ms,
+            "deposition_kernels_ms": post_ms,
+            "flop_per_launch": flop0,
+        },
+        "beam": {
+            "call_ms": ms_per_step,
+            "device0_trace_ms": kern_ms,
+            "device0_deposition_ms": post_ms,
+            "fanout_reduce_only_ms": reduce_ms,
+            "dP_shell_max_diff_between_devices": agree,
+            "deposited_power_sum": float(dP0[-1]),
+        },
+    }
+    print(json.dumps(out), flush=True)
+
+
 def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps, pos, s0):
     """PCIe-inclusive rate of the host-pointer boundary (torj_trace: device
     allocation, H2D of the start states, the trace, D2H of state, status,
@@ -493,7 +685,12 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
                   "worst_tau_ray": {"fan_index": int(idx[int(et.argmax())]),
                                     "tau_gpu": float(gs[int(et.argmax()), 6]),
                                     "tau_cpu": float(os_[int(et.argmax()), 6])},
-                  "bar": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)}
+                  "bar_rel": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10),
+                  "bar": (f"x, N: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} relative to "
+                          f"|x|, |N|; tau: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} "
+                          f"relative, i.e. {1e-6 * {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10):g} "
+                          f"absolute below tau = 1e-6 (the floor: P moves by < 1 ulp there); status "
+                          f"and steps exact")}
         if model == 2:
             parity["note"] = ("weakly relativistic: tau accumulated at Te < 1 keV (cold-edge "
                               "harmonic crossings) is conditioning-limited -- the fsup recurrence "

@@ -34,7 +34,8 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 4  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters */
+#define TORJ_ABI_VERSION 5  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
+                               5: torj_trace_beam_device */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -241,12 +242,42 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
  * communicator from ncclCommInitAll, kept on the handle; n_gpus = 1 needs no
  * reduce unless env TORJ_BEAM_RCCL=1).  Per-ray outputs equal torj_trace_ex's
  * for the same rays and scheduling; dP_shell differs by summation order only.
- * Errors name the failing device. */
+ * Errors name the failing device.  Test-only: env TORJ_BEAM_SAME_DEVICE=1 puts
+ * every replica on p's own device (the threaded multi-replica branch on one
+ * GPU; the partials are then summed on the host, RCCL refusing a device twice). */
 int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                     const double *N0, const double *weights, int n_psi, const double *psi_grid,
                     const double *x_launch, const double *s0, double *state, int *status,
                     int *steps, double *dP_shell, double *P_dep, double *traj, int n_gpus,
                     int n_shards);
+
+/* make_beam's fan-out over DEVICE-RESIDENT shards (the serving / benchmark
+ * form of torj_trace_beam: inputs already in HBM, no host staging).  Shard k
+ * lives on replica k's device -- (p's device + k) mod the device count -- and
+ * its pointers are that device's memory, laid out exactly as the arguments of
+ * torj_trace_device_ex.  Each replica traces its shard on its own stream from
+ * its own host thread (n = 0: nothing), waits and checks it (torj_trace_check);
+ * then, with deposition (n_psi >= 2, psi_grid and dP_shell on every shard),
+ * the (n_psi + 1) dP_shell vectors are all-reduced in place by RCCL, so every
+ * shard's dP_shell holds the sum over the shards (zero them first: the trace
+ * accumulates into them).  n_gpus = 1 skips the reduce unless env
+ * TORJ_BEAM_RCCL=1.  Synchronous.  Same reference interface as torj_trace_beam
+ * (src/solve.jl:209-240). */
+typedef struct {
+    int n;                                    /* rays in this shard */
+    const double *x0, *N0;                    /* 3 x n */
+    const double *weights;                    /* n or NULL */
+    const double *psi_grid;                   /* n_psi (this device's copy) */
+    const double *x_launch, *s0;              /* 3 x n, n (deposition = 1) or NULL */
+    double *state;                            /* 7 x n */
+    int *status, *steps;                      /* n */
+    double *dP_shell;                         /* n_psi + 1, accumulated, then all-reduced */
+    double *P_dep;                            /* n or NULL */
+    double *traj;                             /* (n_steps / traj_stride) x 5 x n or NULL */
+    uint64_t *counters;                       /* 8 or NULL (torj_trace_device) */
+} torj_beam_shard;
+int torj_trace_beam_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n_gpus, int n_psi,
+                           const torj_beam_shard *shards);
 
 /* Scheduling of torj_trace / torj_trace_device launches on this plasma handle
  * (no reference counterpart: an MI355X tuning knob; results are independent

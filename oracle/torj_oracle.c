@@ -868,6 +868,10 @@ double or_alpha_approx(const or_plasma *p, const double x[3], const double N[3],
 /* ------------------------------------------------------------------------- */
 /* launch fan, src/launch.jl:24-132                                          */
 /* ------------------------------------------------------------------------- */
+/* Julia's round(Int64, x), src/launch.jl:81: RoundNearest, halfway cases to
+ * the even integer (lround would round them away from zero) */
+long or_round_int(double x) { return (long)nearbyint(x); }
+
 static void launch_rings(int N_rings, int min_az, double w, double *r_pts, double *r_w,
                          int *N_theta) {
     int n = 2 * N_rings + 2;
@@ -878,7 +882,7 @@ static void launch_rings(int N_rings, int min_az, double w, double *r_pts, doubl
         r_w[i] = wt[N_rings + 1 + i] * (w / sqrt(2.0));
     }
     for (int i = 0; i < N_rings; i++) {
-        long k = lround(min_az * r_pts[i] / r_pts[0]);
+        long k = or_round_int(min_az * r_pts[i] / r_pts[0]);
         N_theta[i] = k < 1 ? 1 : (int)k;
     }
     free(x);

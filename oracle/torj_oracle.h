@@ -123,6 +123,7 @@ typedef double (*or_alpha_fn)(double, double, double, double, double, double, do
 void or_set_alpha_hook(or_alpha_fn fn);
 
 /* ---- launch, src/launch.jl:24-132 and IMAS.pol_tor_angles_2_vector ---- */
+long or_round_int(double x); /* Julia round(Int64, x): ties to even (src/launch.jl:81) */
 int or_launch_count(int N_rings, int min_az);
 int or_launch_peripheral_rays(const double x0[3], const double N0[3], double w,
                               double inv_curv, double f, int N_rings, int min_az,

@@ -29,6 +29,9 @@ void wh_ssbi(double z, int n, int l, double *out) {
 
 int wh_larmornumber(double yg, double npl, double mu) { return torj::larmornumber(yg, npl, mu); }
 
+// the product's Julia round(Int64, x) (launch ring point counts, src/launch.jl:81)
+long wh_round_ties_even(double x) { return torj::round_ties_even(x); }
+
 void wh_alpha_warm(int n, const double *om, const double *X, const double *Y, const double *Nabs,
                    const double *Npar, const double *Te, const double *inv, int mode, int iwarm,
                    double *alpha, double *n2) {

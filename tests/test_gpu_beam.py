@@ -101,5 +101,176 @@ def test_make_beam_traj_stride_keeps_final_state(gpu, T, eq):
     assert pa1 == pa7 and np.array_equal(d1, d7)
     for i in range(len(w1)):
         assert p7[i][-1] == p1[i][-1] and np.array_equal(t7[i][-1], t1[i][-1])
-        assert abs(a7[i][-1] - a1[i][-1]) <= 1e-12
+        # the appended final arc length is the kernel's single-rounding fma
+        assert a7[i][-1] == a1[i][-1]
         assert np.array_equal(p7[i][2:-1], p1[i][2:][6::7][:len(p7[i]) - 3])
+
+
+class _env:
+    """Set environment variables for a block (the library reads these per call)."""
+
+    def __init__(self, **kv):
+        self.kv, self.old = kv, {}
+
+    def __enter__(self):
+        for k, v in self.kv.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+        return self
+
+    def __exit__(self, *exc):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("deposition", ["reference", "binned"])
+def test_trace_beam_threaded_replicas_on_one_device(gpu, T, hplasma, deposition):
+    """The multi-replica branch of torj_trace_beam -- one std::thread, stream and
+    workspace per replica, the branch make_beam(...; n_gpus = 8) takes -- run on
+    one MI355X with the test-only placement TORJ_BEAM_SAME_DEVICE=1 (both
+    replicas on device 0, partials summed on the host).  Per-ray outputs
+    bit-identical to the unsplit launch, dP_shell to its summation order."""
+    pos, xp, Np, s0, w, om = _beam(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, psi_grid=np.linspace(0, 1, 1000), weights=w, traj_stride=100,
+              deposition=deposition, x_launch=pos, s0=s0)
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        with _env(TORJ_BEAM_SAME_DEVICE="1"):
+            b = T.trace(hplasma, xp, Np, om, 1, n_gpus=2, n_shards=5, **kw)
+            c = T.trace(hplasma, xp, Np, om, 1, n_gpus=3, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    _same(a, b)
+    _same(a, c)
+    assert b.dP_shell[-1] > 0
+
+
+def _device_shards(torch, T, plasma, cfg, n_psi, grid, xp, Np, w, pos, s0, cuts, dev):
+    """Device-resident shards for torj_trace_beam_device (all on `dev`)."""
+    n_save = cfg.n_steps // cfg.traj_stride if cfg.traj_stride > 0 else 0
+
+    def d(a, dtype=torch.float64):
+        return torch.from_numpy(np.ascontiguousarray(a)).to(dev, dtype=dtype)
+
+    shards = []
+    for sl in cuts:
+        m = sl.stop - sl.start
+        shards.append(dict(
+            n=m, x0=d(xp[sl].T), N0=d(Np[sl].T), weights=d(w[sl]), psi_grid=d(grid),
+            x_launch=d(pos[sl].T), s0=d(s0[sl]),
+            state=torch.empty((7, m), dtype=torch.float64, device=dev),
+            status=torch.empty(m, dtype=torch.int32, device=dev),
+            steps=torch.empty(m, dtype=torch.int32, device=dev),
+            dP_shell=torch.zeros(n_psi + 1, dtype=torch.float64, device=dev),
+            P_dep=torch.empty(m, dtype=torch.float64, device=dev),
+            traj=torch.empty((max(n_save, 1), 5, m), dtype=torch.float64, device=dev) if n_save else None,
+            counters=torch.zeros(8, dtype=torch.int64, device=dev)))
+    return shards
+
+
+def test_trace_beam_device_shards_threaded(gpu, T, hplasma):
+    """torj_trace_beam_device (device-resident shards, the bench's multi-GPU
+    library path) with three replicas on device 0 (TORJ_BEAM_SAME_DEVICE=1):
+    each shard's outputs bit-identical to the unsplit torj_trace_ex launch of
+    the same rays, every shard's dP_shell = the beam's sum after the reduce,
+    and the work counters add up to the unsplit launch's."""
+    import torch
+
+    from torj_hip._lib import TraceCfg
+    from torj_hip.parallel import group_shard, trace_beam_device
+
+    pos, xp, Np, s0, w, om = _beam(T, hplasma)
+    n = len(w)
+    grid = np.linspace(0, 1, 1000)
+    kw = dict(ds=1e-4, n_steps=2000, psi_grid=grid, weights=w, traj_stride=100,
+              deposition="reference", x_launch=pos, s0=s0)
+    cfg = TraceCfg(om, 1, 1e-4, 2000, 20, 1.0, 1e-6, 1, 100, 1)
+    dev = torch.device("cuda", 0)
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        cuts = [group_shard(n, 3, k) for k in range(3)]
+        sh = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0, cuts, dev)
+        with _env(TORJ_BEAM_SAME_DEVICE="1"):
+            trace_beam_device(hplasma, cfg, len(grid), sh)
+        c1 = torch.zeros(8, dtype=torch.int64, device=dev)
+        one = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0, [slice(0, n)], dev)
+        one[0]["counters"] = c1
+        trace_beam_device(hplasma, cfg, len(grid), one)
+    finally:
+        hplasma.set_sched(-1)
+    for sl, s in zip(cuts, sh):
+        assert np.array_equal(s["state"].cpu().numpy().T, a.state[sl])
+        assert np.array_equal(s["status"].cpu().numpy(), a.status[sl])
+        assert np.array_equal(s["steps"].cpu().numpy(), a.steps[sl])
+        assert np.array_equal(s["P_dep"].cpu().numpy(), a.P_dep[sl])
+        assert np.array_equal(s["traj"].cpu().numpy().transpose(2, 0, 1), a.traj[sl], equal_nan=True)
+        d = s["dP_shell"].cpu().numpy()
+        assert np.abs(d - a.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
+    tot = sum(s["counters"].cpu().numpy() for s in sh)
+    assert np.array_equal(tot, c1.cpu().numpy()) and tot[0] == int(a.steps.sum())
+    assert np.array_equal(one[0]["dP_shell"].cpu().numpy(), a.dP_shell)
+
+
+def test_trace_beam_two_devices(gpu, T, hplasma):
+    """n_gpus = 2 on two real devices (skipped on a one-GPU box): RCCL
+    all-reduce over xGMI, per-ray bit-identical to the unsplit launch."""
+    if gpu < 2:
+        pytest.skip(f"needs two HIP devices, {gpu} visible")
+    pos, xp, Np, s0, w, om = _beam(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, psi_grid=np.linspace(0, 1, 1000), weights=w, traj_stride=100,
+              deposition="reference", x_launch=pos, s0=s0)
+    try:
+        hplasma.set_sched(0)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        b = T.trace(hplasma, xp, Np, om, 1, n_gpus=2, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    _same(a, b)
+
+
+def test_c4_million_ray_beam_sharded_rccl_batched(gpu, T, hplasma, oplasma):
+    """C4 (BASELINE configs[3]) on one MI355X: the 1 005 293-ray fan
+    (N_rings = 291, min_az = 11), 2 000 RK4 steps, Albajar, the reference
+    deposition on 1 000 shells, through make_beam's library path
+    torj_trace_beam with 8 shards, the RCCL reduce forced (TORJ_BEAM_RCCL=1) and
+    the per-launch workspace capped at 4 GiB (TORJ_WS_GB) so every shard runs in
+    ray batches.  Every 250th ray vs the CPU oracle at the parity bar (status
+    and steps exact, x, N, tau 1e-10); per-ray outputs bit-identical to one
+    unsplit torj_trace_ex launch of the beam (its own 16 GiB batches; both on the
+    split pipeline, forced by set_sched(3), so every wave holds the same rays),
+    dP_shell to its summation order."""
+    from test_gpu_parity import _compare_trace
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    f = s["f_abs_test"]
+    om = 2 * np.pi * f
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=291,
+                                            min_azimuthal_points=11)
+    assert len(w) == 1005293
+    xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1, gpu=True)
+    assert (st == T.OK).all()
+    grid = np.linspace(0.0, 1.0, 1000)
+    kw = dict(ds=1e-4, n_steps=2000, psi_grid=grid, weights=w, traj_stride=500,
+              deposition="reference", x_launch=pos, s0=s0)
+    try:
+        hplasma.set_sched(3)
+        a = T.trace(hplasma, xp, Np, om, 1, **kw)
+        with _env(TORJ_BEAM_RCCL="1", TORJ_WS_GB="4"):
+            b = T.trace(hplasma, xp, Np, om, 1, n_gpus=1, n_shards=8, **kw)
+    finally:
+        hplasma.set_sched(-1)
+    _same(a, b)
+    idx = np.arange(0, len(w), 250)
+    o = oplasma.trace(xp[idx], Np[idx], om, 1, 1e-4, 2000, psi_grid=grid, weights=w[idx])
+    sub = type(b)(b.state[idx], b.status[idx], b.steps[idx], None, None, None)
+    _compare_trace(sub, o)
+    assert abs(b.dP_shell[-1] - np.dot(w, b.P_dep)) <= 1e-12 * b.dP_shell[-1]
+    assert np.median(b.P_end) < 0.1  # the X2 layer absorbs most of the beam

@@ -56,6 +56,30 @@ def test_launch_defaults_and_argument_error(O):
     assert O.lib().or_launch_count(14, 5) == 1038
 
 
+def test_launch_rounding_is_julias_ties_to_even(O):
+    """round(Int64, min_azimuthal_points * r_pts[i] / r_pts[1]) (src/launch.jl:81)
+    is Julia's RoundNearest: halfway cases go to the even integer (C's lround
+    would round them away from zero).  Checked at constructed exact halves in the
+    oracle and in the product's host build (torj_math.hpp round_ties_even)."""
+    import ctypes as C
+    import os
+    import subprocess
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.check_call(["make", "-s", "-C", os.path.join(here, "native"), "build/libwarm_host.so"])
+    H = C.CDLL(os.path.join(here, "native", "build", "libwarm_host.so"))
+    H.wh_round_ties_even.restype = C.c_long
+    H.wh_round_ties_even.argtypes = [C.c_double]
+    O.lib().or_round_int.restype = C.c_long
+    O.lib().or_round_int.argtypes = [C.c_double]
+    cases = {0.5: 0, 1.5: 2, 2.5: 2, 3.5: 4, 4.5: 4, 10.5: 10, 11.5: 12, 2.4999999999999996: 2,
+             2.5000000000000004: 3, 1.0: 1, 0.49999999999999994: 0, -0.5: 0, -1.5: -2}
+    for x, want in cases.items():
+        assert O.lib().or_round_int(x) == want, x
+        assert H.wh_round_ties_even(x) == want, x
+        assert round(x) == want  # Python 3's round is the same convention
+
+
 # ---------------------------------------------------------------- splines
 def test_bspline_line_ongrid_equals_natural_cubic_spline(O):
     """Cubic(Line(OnGrid())) = C2 cubic interpolant with zero 2nd derivative at

@@ -896,6 +896,9 @@ struct SplitArgs {
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
 };
 
+// steps | status << 24: split launches need n_steps < kSplitMaxSteps (the
+// fused kernels have no such limit and take longer traces)
+constexpr int kSplitMaxSteps = 1 << 24;
 __device__ __forceinline__ int info_steps(int v) { return v & 0xffffff; }
 __device__ __forceinline__ int info_status(int v) { return (unsigned)v >> 24; }
 __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st << 24); }
@@ -1010,7 +1013,13 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
             N[c] = sp.tx[(3 + c) * (size_t)a.n + i];
         }
     }
-    // a ray the scan has stopped (ABSORBED) needs no more trajectory (stale reads are harmless)
+    // a ray the scan has stopped (ABSORBED) needs no more trajectory.  sinfo is
+    // written by k_tau_scan on another stream while this kernel may run, so the
+    // read can be stale.  INVARIANT: this early-out only saves work, it never
+    // decides an output -- a stale OK just traces steps nobody reads (the scan
+    // stopped first; k_split_final rebuilds the state from the chunk-boundary
+    // copy and the scan's carry).  Keep it that way: tests/test_gpu_split.py
+    // test_split_serial_equals_overlapped holds both orders bit-identical.
     if (st != ST_OK || (sp.k0 > 0 && info_status(sp.sinfo[i]) != ST_OK)) return;
     const int s_end = min(a.n_steps, sp.k0 + sp.kb);
     for (int s = steps; s < s_end; s++) {
@@ -1085,6 +1094,9 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     if (i >= a.n) return;
     const int j = js >> 2;
     const int ti = sp.tinfo[i];
+    // sinfo may be stale (k_tau_scan of an earlier block runs on another
+    // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
+    // alpha the scan never reads
     if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
     const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
     AlbajarWork work = {};
@@ -1876,8 +1888,8 @@ static Rings make_rings(int N_rings, int min_az, double w) {
         R.r.push_back(x[N_rings + 1 + i] * (w / std::sqrt(2.0)));
         R.rw.push_back(wt[N_rings + 1 + i] * (w / std::sqrt(2.0)));
     }
-    for (int i = 0; i < N_rings; i++) {  // :80-83
-        const long k = std::lround(min_az * R.r[i] / R.r[0]);
+    for (int i = 0; i < N_rings; i++) {  // :80-83, Julia's round(Int64, x): ties to even
+        const long k = round_ties_even(min_az * R.r[i] / R.r[0]);
         R.nth.push_back(k < 1 ? 1 : (int)k);
         R.total += R.nth.back();
     }
@@ -2345,10 +2357,15 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // steps per block: kRing alpha-input buffers within the budget (TORJ_SPLIT_MB
     // per buffer, default 1024: measured 66.5 / 67.8 / 69.4 ms at 1 / 2 / 4 GiB on
     // the headline beam), a multiple of the chunk length
-    static const size_t budget = [] {
+    static const size_t budget_env = [] {
         const char *e = getenv("TORJ_SPLIT_MB");
         return (size_t)(e ? atol(e) : 1024) << 20;
     }();
+    // ... and at most 1/16 of the device memory free now for each of the kRing
+    // buffers (a quarter of it for the whole ring; 1 GiB on an idle MI355X)
+    size_t free_b = 0, total_b = 0;
+    HIPCK(hipMemGetInfo(&free_b, &total_b));
+    const size_t budget = std::max<size_t>(std::min(budget_env, free_b / 16), 1);
     constexpr int R = torj_plasma_s::kRing;
     const int nf = a.abs_model >= 2 ? kAinFW : kAinF;
     const size_t per_step = 4 * (size_t)nf * sizeof(double) * n;
@@ -2358,8 +2375,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     kb = std::min<long>(kb, n_steps);
     const int n_cb = (a.chunk_steps > 0 ? n_steps / a.chunk_steps : 0) + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    // work words exist only for a counted launch (a.counters): uncounted
+    // (production) launches neither write nor read them, nor reserve them
     const size_t b_ain = al(per_step * kb), b_alpha = al(4 * sizeof(double) * n * kb),
-                 b_awork = al(4 * sizeof(unsigned) * n * kb),
+                 b_awork = a.counters ? al(4 * sizeof(unsigned) * n * kb) : 0,
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
     const int nq = (int)((n + 255) / 256);
@@ -2393,10 +2412,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     sp.tinfo = (int *)take(b_n4);
     sp.sinfo = (int *)take(b_n4);
 
-    static const bool serial = [] {  // TORJ_SPLIT_SERIAL=1: no overlap (measurement aid)
-        const char *e = getenv("TORJ_SPLIT_SERIAL");
-        return e && atoi(e) != 0;
-    }();
+    // TORJ_SPLIT_SERIAL=1: every kernel on the caller's stream, no overlap (a
+    // measurement aid; read per call so a test can compare both orders)
+    const char *serial_e = getenv("TORJ_SPLIT_SERIAL");
+    const bool serial = serial_e && atoi(serial_e) != 0;
     // the scan on a third stream (TORJ_SPLIT_SCAN=0: behind the alpha kernel on
     // the second), so the alpha kernel of block b + 1 need not wait for the
     // latency-bound one-lane-per-ray scan of block b
@@ -2448,7 +2467,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.ain = ain[r];
         sp.psib = psib[r];
         sp.alpha = alphas[r];
-        sp.awork = a.counters ? aworks[r] : nullptr;  // work words only for a counted launch
+        sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
         if (lds_traj)
@@ -2791,7 +2810,9 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     const bool warm_split = cfg->absorption >= 2 && split_env == 1 &&
                             (split_warm_env == 1 ||
                              (split_warm_env < 0 && (cfg->absorption == 2 || G < p->n_cu * 3)));
+    // (the split kernels pack a ray's step count into 24 bits beside its status)
     const bool use_split = !adaptive && cfg->absorption >= 1 && cfg->n_steps > 0 &&
+                           cfg->n_steps < kSplitMaxSteps &&
                            (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
     if (use_split) {
         if (split_trace(p, a, DM, tr, cs, s)) return -1;
@@ -2996,19 +3017,41 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
     return torj_trace_check(p, s);
 }
 
+}  // extern "C"
+
 // ---- make_beam across the GPUs of this process (src/solve.jl:209-240) -----
 // Replica k of a plasma handle: the same coefficients on device (device + k)
 // mod the device count, with its own stream, scratch and scheduling copy.
-static int beam_replicas(torj_plasma_s *p, int n_gpus) {
+//
+// Test-only placement: env TORJ_BEAM_SAME_DEVICE=1 (read per call) puts every
+// replica on the handle's own device, so the multi-replica branch -- one host
+// thread, stream and workspace per replica -- runs on a one-GPU machine.  RCCL
+// rejects a communicator with a device twice, so those partials are summed on
+// the host, in replica order, instead of by the all-reduce.
+static bool beam_same_device() {
+    const char *e = getenv("TORJ_BEAM_SAME_DEVICE");
+    return e && atoi(e) != 0;
+}
+
+static int beam_replicas(torj_plasma_s *p, int n_gpus, bool same) {
     int ndev = 0;
     HIPCK(hipGetDeviceCount(&ndev));
-    if (n_gpus < 1 || n_gpus > ndev)
+    if (n_gpus < 1 || (!same && n_gpus > ndev))
         return fail("n_gpus = %d, but %d HIP devices are visible", n_gpus, ndev);
     std::lock_guard<std::mutex> lk(p->mu);
     if (p->replicas.empty()) p->replicas.push_back(p);
+    auto dev_of = [&](size_t k) { return same ? p->device : (p->device + (int)k) % ndev; };
+    for (size_t k = 1; k < p->replicas.size(); k++)
+        if (p->replicas[k]->device != dev_of(k)) {  // placement changed: rebuild them all
+            for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
+            p->comms.clear();
+            for (size_t j = 1; j < p->replicas.size(); j++) torj_plasma_destroy(p->replicas[j]);
+            p->replicas.resize(1);
+            break;
+        }
     while ((int)p->replicas.size() < n_gpus) {
         auto *q = new torj_plasma_s();
-        q->device = (p->device + (int)p->replicas.size()) % ndev;
+        q->device = dev_of(p->replicas.size());
         q->g = p->g;
         q->coef = p->coef;
         q->n_vol = p->n_vol;
@@ -3022,6 +3065,82 @@ static int beam_replicas(torj_plasma_s *p, int n_gpus) {
         p->replicas[k]->sched_mode = p->sched_mode;
         p->replicas[k]->sched_waves = p->sched_waves;
         p->replicas[k]->lanes_per_ray = p->lanes_per_ray;
+    }
+    return 0;
+}
+
+// Run f(k) for k < n_gpus: inline for one replica, else one host thread per
+// replica (each drives its own device and stream).  Returns the first failure,
+// naming its device.
+template <class F>
+static int beam_fanout(torj_plasma_s *p, int n_gpus, const char *what, F &&f) {
+    std::vector<std::string> errs(n_gpus);
+    std::vector<int> rc(n_gpus, 0);
+    auto run = [&](int k) {
+        rc[k] = -1;
+        if (hipSetDevice(p->replicas[k]->device) != hipSuccess) {
+            errs[k] = "hipSetDevice failed";
+            return;
+        }
+        rc[k] = f(k);
+        if (rc[k]) errs[k] = g_err;
+    };
+    if (n_gpus == 1) {
+        run(0);
+    } else {
+        std::vector<std::thread> th;
+        for (int k = 0; k < n_gpus; k++) th.emplace_back(run, k);
+        for (auto &t : th) t.join();
+    }
+    for (int k = 0; k < n_gpus; k++)
+        if (rc[k]) return fail("%s, device %d: %s", what, p->replicas[k]->device, errs[k].c_str());
+    return 0;
+}
+
+// make_beam's reduce (src/solve.jl:233-240): d_dP[k] (n_psi + 1 fp64 on replica
+// k's device) <- sum over k, in place on every replica (all-reduce semantics).
+// RCCL over xGMI from a single-process communicator (ncclCommInitAll, kept on
+// the handle) enqueued on the replicas' streams; the test-only same-device
+// placement sums on the host.  Synchronous: the replicas' streams are drained.
+static int beam_reduce(torj_plasma_s *p, int n_gpus, const std::vector<double *> &d_dP, int n_psi,
+                       bool same) {
+    const size_t m = (size_t)n_psi + 1;
+    if (same) {
+        std::vector<double> acc(m, 0.0), part(m);
+        for (int k = 0; k < n_gpus; k++) {
+            torj_plasma_s *q = p->replicas[k];
+            HIPCK(hipSetDevice(q->device));
+            HIPCK(hipMemcpyAsync(part.data(), d_dP[k], m * sizeof(double), hipMemcpyDeviceToHost, q->stream));
+            HIPCK(hipStreamSynchronize(q->stream));
+            for (size_t j = 0; j < m; j++) acc[j] += part[j];
+        }
+        for (int k = 0; k < n_gpus; k++) {
+            torj_plasma_s *q = p->replicas[k];
+            HIPCK(hipSetDevice(q->device));
+            HIPCK(hipMemcpyAsync(d_dP[k], acc.data(), m * sizeof(double), hipMemcpyHostToDevice, q->stream));
+            HIPCK(hipStreamSynchronize(q->stream));
+        }
+        return 0;
+    }
+    if ((int)p->comms.size() != n_gpus) {
+        for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
+        p->comms.assign(n_gpus, nullptr);
+        std::vector<int> devs(n_gpus);
+        for (int k = 0; k < n_gpus; k++) devs[k] = p->replicas[k]->device;
+        if (ncclCommInitAll(p->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
+            p->comms.clear();
+            return fail("ncclCommInitAll over %d devices failed", n_gpus);
+        }
+    }
+    ncclResult_t r = ncclGroupStart();
+    for (int k = 0; k < n_gpus && r == ncclSuccess; k++)
+        r = ncclAllReduce(d_dP[k], d_dP[k], m, ncclDouble, ncclSum, p->comms[k], p->replicas[k]->stream);
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+        return fail("ncclAllReduce of dP_shell failed: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (int k = 0; k < n_gpus; k++) {
+        HIPCK(hipSetDevice(p->replicas[k]->device));
+        HIPCK(hipStreamSynchronize(p->replicas[k]->stream));
     }
     return 0;
 }
@@ -3104,6 +3223,8 @@ static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S
     return 0;
 }
 
+extern "C" {
+
 int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const double *x0,
                     const double *N0, const double *weights, int n_psi, const double *grid,
                     const double *x_launch, const double *s0, double *state, int *status,
@@ -3121,73 +3242,27 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
             if (!(grid[k] > grid[k - 1])) return fail("psi_dP_dV must be strictly increasing");
         if (!dP || !Pdep) return fail("deposition needs dP_shell and P_dep");
     }
-    if (beam_replicas(p, n_gpus)) return -1;
+    const bool same = beam_same_device();
+    if (beam_replicas(p, n_gpus, same)) return -1;
     const int S = std::max(n_shards > 0 ? n_shards : n_gpus, n_gpus);
     const char *rccl_e = getenv("TORJ_BEAM_RCCL");  // read per call (tests toggle it)
-    const bool rccl_env = rccl_e && atoi(rccl_e) != 0;
-    const bool rccl = depo && (n_gpus > 1 || rccl_env);
-    // per-device partial dP_shell, reduced by one RCCL all-reduce
+    const bool reduce = depo && (n_gpus > 1 || (rccl_e && atoi(rccl_e) != 0));
+    // per-device partial dP_shell, then one all-reduce
     std::vector<double *> d_dP(n_gpus, nullptr);
-    std::vector<std::string> errs(n_gpus);
-    std::vector<int> rc(n_gpus, 0);
-    auto run = [&](int k) {
+    int out = beam_fanout(p, n_gpus, "torj_trace_beam", [&](int k) -> int {
         torj_plasma_s *q = p->replicas[k];
-        rc[k] = -1;
-        if (hipSetDevice(q->device) != hipSuccess) {
-            errs[k] = "hipSetDevice failed";
-            return;
-        }
-        if (depo && hipMalloc(&d_dP[k], (n_psi + 1) * sizeof(double)) != hipSuccess) {
-            errs[k] = "hipMalloc of the dP_shell partial failed";
-            return;
-        }
-        rc[k] = beam_worker(q, cfg, n, S, k, n_gpus, x0, N0, weights, n_psi, grid, x_launch, s0,
-                            state, status, steps, depo ? Pdep : nullptr, traj, d_dP[k]);
-        if (rc[k]) errs[k] = g_err;
-    };
-    if (n_gpus == 1) {
-        run(0);
-    } else {  // one host thread per device: each drives its own stream
-        std::vector<std::thread> th;
-        for (int k = 0; k < n_gpus; k++) th.emplace_back(run, k);
-        for (auto &t : th) t.join();
-    }
-    int out = 0;
-    for (int k = 0; k < n_gpus && !out; k++)
-        if (rc[k]) out = fail("torj_trace_beam, device %d: %s", p->replicas[k]->device, errs[k].c_str());
+        if (depo) HIPCK(hipMalloc(&d_dP[k], (n_psi + 1) * sizeof(double)));
+        return beam_worker(q, cfg, n, S, k, n_gpus, x0, N0, weights, n_psi, grid, x_launch, s0, state,
+                           status, steps, depo ? Pdep : nullptr, traj, d_dP[k]);
+    });
+    if (!out && reduce) out = beam_reduce(p, n_gpus, d_dP, n_psi, same);
     if (!out && depo) {
-        if (rccl) {
-            // make_beam's reduce (src/solve.jl:233-240): sum of the (n_psi+1)
-            // partials over the devices, RCCL over xGMI, single-process communicator
-            if ((int)p->comms.size() != n_gpus) {
-                for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
-                p->comms.assign(n_gpus, nullptr);
-                std::vector<int> devs(n_gpus);
-                for (int k = 0; k < n_gpus; k++) devs[k] = p->replicas[k]->device;
-                if (ncclCommInitAll(p->comms.data(), n_gpus, devs.data()) != ncclSuccess) {
-                    p->comms.clear();
-                    out = fail("ncclCommInitAll over %d devices failed", n_gpus);
-                }
-            }
-            if (!out) {
-                ncclResult_t r = ncclGroupStart();
-                for (int k = 0; k < n_gpus && r == ncclSuccess; k++)
-                    r = ncclAllReduce(d_dP[k], d_dP[k], (size_t)n_psi + 1, ncclDouble, ncclSum,
-                                      p->comms[k], p->replicas[k]->stream);
-                const ncclResult_t r2 = ncclGroupEnd();
-                if (r != ncclSuccess || r2 != ncclSuccess)
-                    out = fail("ncclAllReduce of dP_shell failed: %s",
-                               ncclGetErrorString(r != ncclSuccess ? r : r2));
-            }
-        }
-        if (!out) {
-            torj_plasma_s *q0 = p->replicas[0];
-            if (hipSetDevice(q0->device) != hipSuccess ||
-                hipMemcpyAsync(dP, d_dP[0], (n_psi + 1) * sizeof(double), hipMemcpyDeviceToHost,
-                               q0->stream) != hipSuccess ||
-                hipStreamSynchronize(q0->stream) != hipSuccess)
-                out = fail("download of dP_shell failed");
-        }
+        torj_plasma_s *q0 = p->replicas[0];
+        if (hipSetDevice(q0->device) != hipSuccess ||
+            hipMemcpyAsync(dP, d_dP[0], (n_psi + 1) * sizeof(double), hipMemcpyDeviceToHost,
+                           q0->stream) != hipSuccess ||
+            hipStreamSynchronize(q0->stream) != hipSuccess)
+            out = fail("download of dP_shell failed");
     }
     for (int k = 0; k < n_gpus; k++)
         if (d_dP[k]) {
@@ -3198,6 +3273,39 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
     if (!out && !depo) {
         if (dP) std::fill(dP, dP + (n_psi > 0 ? n_psi + 1 : 1), 0.0);
         if (Pdep) std::fill(Pdep, Pdep + n, 0.0);
+    }
+    (void)hipSetDevice(p->device);
+    return out;
+}
+
+int torj_trace_beam_device(torj_plasma_t p, const torj_trace_cfg *cfg, int n_gpus, int n_psi,
+                           const torj_beam_shard *shards) {
+    if (!p || !cfg || !shards) return fail("bad plasma handle, cfg or shards");
+    const bool same = beam_same_device();
+    if (beam_replicas(p, n_gpus, same)) return -1;
+    bool depo = n_psi >= 2;
+    for (int k = 0; k < n_gpus; k++) {
+        if (shards[k].n < 0) return fail("shard %d: n < 0", k);
+        depo = depo && shards[k].psi_grid && shards[k].dP_shell;
+    }
+    if (n_psi >= 2 && !depo) return fail("deposition needs psi_grid and dP_shell on every shard");
+    const char *rccl_e = getenv("TORJ_BEAM_RCCL");
+    const bool reduce = depo && (n_gpus > 1 || (rccl_e && atoi(rccl_e) != 0));
+    int out = beam_fanout(p, n_gpus, "torj_trace_beam_device", [&](int k) -> int {
+        torj_plasma_s *q = p->replicas[k];
+        const torj_beam_shard &h = shards[k];
+        if (ensure_device(q)) return -1;
+        if (h.n > 0 &&
+            torj_trace_device_ex(q, cfg, h.n, h.x0, h.N0, h.weights, depo ? n_psi : 0, h.psi_grid,
+                                 h.x_launch, h.s0, h.state, h.status, h.steps, h.dP_shell, h.P_dep,
+                                 h.traj, h.counters, q->stream))
+            return -1;
+        return torj_trace_check(q, q->stream);  // waits for the stream: queue / grid flags
+    });
+    if (!out && reduce) {
+        std::vector<double *> d_dP(n_gpus);
+        for (int k = 0; k < n_gpus; k++) d_dP[k] = shards[k].dP_shell;
+        out = beam_reduce(p, n_gpus, d_dP, n_psi, same);
     }
     (void)hipSetDevice(p->device);
     return out;

@@ -60,6 +60,12 @@ TORJ_HD void bweights(double d, double w[4], double dw[4]) {
 
 TORJ_HD double clampd(double x, double lo, double hi) { return x > hi ? hi : (x < lo ? lo : x); }
 
+// Julia's round(Int64, x) (RoundNearest: halfway cases to the even integer,
+// e.g. the azimuthal point counts of src/launch.jl:81); C's lround would take
+// them away from zero.  rint rounds in the default (to-nearest-even) mode and
+// is exact for every representable halfway case.
+TORJ_HD long round_ties_even(double x) { return (long)rint(x); }
+
 // 1/x for the denominators of the ray RHS and the absorption prologue: on the
 // device v_rcp_f64 + two Newton steps (<= 1 ulp) instead of the IEEE division
 // sequence (div_scale x2, rcp, five fma, div_fmas, div_fixup per quotient).

@@ -19,7 +19,7 @@ module TorJHIP
 import TorJ
 
 const libtorj = get(ENV, "TORJ_HIP_LIB", joinpath(@__DIR__, "..", "build", "libtorj_hip.so"))
-const ABI_VERSION = 4  # include/torj_hip.h TORJ_ABI_VERSION
+const ABI_VERSION = 5  # include/torj_hip.h TORJ_ABI_VERSION
 
 function __init__()
     v = ccall((:torj_abi_version, libtorj), Cint, ())
@@ -207,6 +207,9 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
     n_steps = max(1, round(Int, s_max / ds))
     cap = integrator == 1 ? 2n_steps + 400 : n_steps
     traj_stride >= 1 || throw(ArgumentError("traj_stride must be >= 1"))
+    # checked before tracing: the adaptive integrator's final state is no saved sample
+    (integrator == 1 && traj_stride > 1) &&
+        throw(ArgumentError("integrator = 1 (adaptive) needs traj_stride = 1"))
     cfg = TraceCfg(ω, mode, ds, cap, max(1, n_steps ÷ 100), 1.0, 1e-6, absorption, traj_stride,
                    deposition, integrator, 1e-6, 1e-6, s_max, 100)
     state, status, steps, dP, Pdep, traj = trace(p, cfg, xp, Np, w, psi_dP_dV, pos, s0;
@@ -218,8 +221,8 @@ function make_beam(p::GPUPlasma, r, phi, z, tor, pol, spot, inv_curv, f, mode::I
         k = steps[i] ÷ traj_stride
         s_i, x_i, τ_i = traj[i, 5, 1:k], [traj[i, 1:3, j] for j in 1:k], traj[i, 4, 1:k]
         if steps[i] % traj_stride != 0  # the final state is not a saved sample
-            integrator == 0 || throw(ArgumentError("traj_stride must divide the step count (adaptive)"))
-            push!(s_i, s0[i] + ds * steps[i]); push!(x_i, state[i, 1:3]); push!(τ_i, state[i, 7])
+            # fma: the single-rounding s0 + steps ds the trajectory kernel stores
+            push!(s_i, fma(Float64(steps[i]), ds, s0[i])); push!(x_i, state[i, 1:3]); push!(τ_i, state[i, 7])
         end
         push!(arc_lengths, vcat(0.0, s0[i], s_i))
         push!(trajectories, vcat([pos[i, :]], [xp[i, :]], x_i))

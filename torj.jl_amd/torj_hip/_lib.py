@@ -41,6 +41,15 @@ class TraceCfg(C.Structure):
                          traj_stride, deposition, integrator, abstol, reltol, s_max, n_chunks)
 
 
+class BeamShard(C.Structure):
+    """torj_beam_shard: one device's shard of torj_trace_beam_device (device pointers)"""
+    _fields_ = [("n", C.c_int), ("x0", C.c_void_p), ("N0", C.c_void_p), ("weights", C.c_void_p),
+                ("psi_grid", C.c_void_p), ("x_launch", C.c_void_p), ("s0", C.c_void_p),
+                ("state", C.c_void_p), ("status", C.c_void_p), ("steps", C.c_void_p),
+                ("dP_shell", C.c_void_p), ("P_dep", C.c_void_p), ("traj", C.c_void_p),
+                ("counters", C.c_void_p)]
+
+
 _SIGS = {
     "torj_abi_version": (C.c_int, []),
     "torj_last_error": (C.c_char_p, []),
@@ -78,6 +87,8 @@ _SIGS = {
                                 _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp]),
     "torj_trace_beam": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, _dp, _dp, _dp, C.c_int,
                                   _dp, _dp, _dp, _dp, _ip, _ip, _dp, _dp, _dp, C.c_int, C.c_int]),
+    "torj_trace_beam_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_int,
+                                         C.POINTER(BeamShard)]),
     "torj_set_sched": (C.c_int, [C.c_void_p, C.c_int, C.c_int]),
     "torj_trace_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),
@@ -92,7 +103,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 4  # include/torj_hip.h TORJ_ABI_VERSION
+ABI_VERSION = 5  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 

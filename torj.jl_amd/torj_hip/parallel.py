@@ -25,3 +25,40 @@ def allreduce_deposition(dP_shell, group=None):
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
         dist.all_reduce(dP_shell, op=dist.ReduceOp.SUM, group=group)
     return dP_shell
+
+
+def group_shard(n: int, n_shards: int, k: int) -> slice:
+    """Shard k of n_shards over n rays with boundaries on 64-ray multiples (one
+    wave / one work-queue group), as torj_trace_beam cuts a beam (beam_shard in
+    torj_hip.hip): every shard holds whole 64-ray groups of the unsplit beam, so
+    per-ray results do not depend on the split."""
+    if n_shards < 1 or not (0 <= k < n_shards):
+        raise ValueError(f"bad shard {k} / {n_shards}")
+    G = (n + 63) // 64
+    lo = min(G * k // n_shards * 64, n)
+    hi = min(G * (k + 1) // n_shards * 64, n)
+    return slice(lo, hi)
+
+
+_SHARD_FIELDS = ("x0", "N0", "weights", "psi_grid", "x_launch", "s0", "state", "status", "steps",
+                 "dP_shell", "P_dep", "traj", "counters")
+
+
+def trace_beam_device(plasma, cfg, n_psi: int, shards) -> None:
+    """torj_trace_beam_device: make_beam's fan-out over device-resident shards
+    (src/solve.jl:209-240).  shards[k] is a dict with "n" and any of the
+    torj_beam_shard fields (torch tensors on replica k's device -- (plasma
+    device + k) mod count -- or raw device pointers); each shard's dP_shell ends
+    as the sum over all shards (RCCL all-reduce).  Synchronous."""
+    from ._lib import BeamShard, TraceCfg, check, lib  # noqa: F401
+    import ctypes as C
+
+    arr = (BeamShard * len(shards))()
+    for k, sh in enumerate(shards):
+        arr[k].n = int(sh["n"])
+        for f in _SHARD_FIELDS:
+            v = sh.get(f)
+            if v is not None and not isinstance(v, int):
+                v = v.data_ptr()
+            setattr(arr[k], f, v)
+    check(lib().torj_trace_beam_device(plasma.handle, C.byref(cfg), len(shards), int(n_psi), arr))

@@ -163,12 +163,19 @@ def make_ray(plasma, x0, N_vacuum, f: float, mode: int, s_max: float, psi_dP_dV,
     return s, u, P_beam, dP_dV, float(r.P_dep[0])
 
 
-def _final_arc_length(res, i, s0, ds, integrator):
-    """Arc length of ray i's final state: s0 + steps * ds for RK4 (the kernel's
-    own fma), not recorded for the adaptive integrator's unsaved last step."""
-    if integrator == "rk4":
-        return s0 + ds * int(res.steps[i])
-    raise ValueError("make_beam: traj_stride must divide the step count with integrator='adaptive'")
+def fma(a: float, b: float, c: float) -> float:
+    """a * b + c with ONE rounding (Python 3.10 has no math.fma): the exact
+    rational value, rounded once by the correctly rounded Fraction -> float."""
+    from fractions import Fraction
+
+    return float(Fraction(a) * Fraction(b) + Fraction(c))
+
+
+def _final_arc_length(res, i, s0, ds):
+    """Arc length of ray i's final RK4 state: fma(steps, ds, s0), the single-
+    rounding product-sum the trajectory kernel stores (its s0 + steps * ds is
+    contracted to one v_fma_f64)."""
+    return fma(float(int(res.steps[i])), float(ds), float(s0))
 
 
 def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
@@ -183,6 +190,10 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
     summed across them (:233-240).  traj_stride > 1 keeps every traj_stride-th
     step of each ray plus its final state, so ray_powers[i][-1] is the ray's
     final P as in the reference."""
+    if integrator == "adaptive" and traj_stride > 1:
+        # checked before any tracing: the adaptive integrator's final state is
+        # not a saved sample and its arc length is not recorded
+        raise ValueError("make_beam: integrator='adaptive' needs traj_stride = 1")
     omega = 2.0 * np.pi * f
     N0 = pol_tor_angles_2_vector(steering_angle_pol, steering_angle_tor)
     x0 = np.array([r * np.cos(phi), r * np.sin(phi), z])
@@ -210,7 +221,7 @@ def make_beam(plasma, r: float, phi: float, z: float, steering_angle_tor: float,
         k = int(res.steps[i]) // traj_stride
         s_i, x_i, tau_i = res.traj[i, :k, 4], res.traj[i, :k, :3], res.traj[i, :k, 3]
         if int(res.steps[i]) % traj_stride:  # the final state is not a saved sample
-            s_end = _final_arc_length(res, i, s0[i], ds, integrator)
+            s_end = _final_arc_length(res, i, s0[i], ds)
             s_i = np.concatenate([s_i, [s_end]])
             x_i = np.vstack([x_i, res.state[i, :3][None]])
             tau_i = np.concatenate([tau_i, [res.state[i, 6]]])
