@@ -212,7 +212,8 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
  * (torj_hip/flops.py): [0] ray-steps, [1] RHS evaluations, then
  *   absorption 1 (Albajar): [2] calls reaching the harmonic sum, [3] harmonic
  *     integrals evaluated, [4] Bessel-series terms, [5] harmonic integrals found
- *     exactly zero without their node loop, [6] [7] 0;
+ *     exactly zero without their node loop, [6] harmonic integrals skipped as
+ *     provably below an ulp of the sum (alpha bit-identical), [7] 0;
  *   absorption 2 (warm, iwarm 1): [2] larmornumber tests, [3] Faddeeva
  *     evaluations, [4] warmdisp passes, [5] passes x Larmor order lrm,
  *     [6] sum lrm, [7] sum lrm^2 (one warm alpha per RHS evaluation);

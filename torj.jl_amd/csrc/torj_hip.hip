@@ -394,7 +394,9 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
     const unsigned long long s3 = wave_sum((unsigned long long)work.n_harm);
     const unsigned long long s4 = wave_sum((unsigned long long)work.n_terms);
     const unsigned long long s5 = wave_sum((unsigned long long)work.n_zero);
-    const unsigned long long s6 = wave_sum((unsigned long long)work.n_l);
+    // [6]: Albajar's negligible-harmonic skips, or the warm model's sum of lrm
+    // (each model leaves the other's field 0)
+    const unsigned long long s6 = wave_sum((unsigned long long)(work.n_l + work.n_negl));
     const unsigned long long s7 = wave_sum((unsigned long long)work.n_l2);
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(a.counters + 0, s0);
@@ -883,7 +885,8 @@ struct SplitArgs {
     double *ain;          // [j][stage][f][n]: this block's alpha inputs, nf fields
     double *alpha;        // [j][stage][n]
     unsigned *awork;      // [j][stage][n] (null unless counted): alpha work counts; Albajar: bit 0 active,
-                          // bits 1-2 harmonics, 3-4 exact-zero harmonics, 5-15 Bessel terms;
+                          // bits 1-2 harmonics, 3-4 exact-zero harmonics, 5-15 Bessel terms,
+                          // 16-17 negligible harmonics;
                           // warm: bits 0-6 larmornumber tests, 7-13 Faddeeva evaluations,
                           // 14-20 warmdisp passes, 21-23 Larmor order
     double *psib;         // binned deposition: psi at the end of step k0 + j, [j][n]
@@ -1106,7 +1109,8 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     sp.alpha[(size_t)js * a.n + i] = al;
     if (sp.awork)  // a counted launch (null otherwise: no work words written or read)
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
-                                     ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5);
+                                     ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
+                                     ((work.n_negl & 3u) << 16);
 }
 
 // the warm alpha (absorption 2 / 3, iwarm 1 / 3) at the stored stage points:
@@ -1203,7 +1207,8 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
                         c2 += wk & 1u;
                         c3 += (wk >> 1) & 3u;
                         c5 += (wk >> 3) & 3u;
-                        c4 += wk >> 5;
+                        c4 += (wk >> 5) & 2047u;
+                        c6 += (wk >> 16) & 3u;
                     } else if (am == 2) {
                         const unsigned lrm = wk >> 21, passes = (wk >> 14) & 127u;
                         c2 += wk & 127u;
@@ -1915,6 +1920,11 @@ int torj_abs_al_init(int n) {
     std::lock_guard<std::mutex> lk(g_gl_mu);
     GLTable t{};
     t.n = n;
+    // the bit-identical skip of provably negligible harmonic integrals
+    // (torj_math.hpp albajar_harmonic); env TORJ_NEGL_SKIP=0 turns it off (A/B
+    // and the test that holds both bit-identical), read at each abs_Al_init
+    const char *ne = getenv("TORJ_NEGL_SKIP");
+    t.negl_skip = ne ? (atoi(ne) != 0) : 1;
     gauss_legendre(n, t.t, t.w);
     for (int i = 0; i < n; i++) {
         t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);

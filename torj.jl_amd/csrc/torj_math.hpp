@@ -493,6 +493,7 @@ constexpr double series_coef(int nu, int k) { return inv_fact(k) * inv_fact(k + 
 
 struct GLTable {
     int n;
+    int negl_skip;  // 1: skip harmonic integrals provably below an ulp of the sum (default)
     double t[kMaxGL], w[kMaxGL], st[kMaxGL], t2[kMaxGL];  // nodes, weights, sqrt(1-t^2), t^2
 };
 
@@ -738,6 +739,7 @@ struct AlbajarWork {
     uint32_t n_zero;    // harmonic integrals found exactly zero / passes x Larmor order
     uint32_t n_l;       // - / sum of Larmor orders lrm
     uint32_t n_l2;      // - / sum of lrm^2
+    uint32_t n_negl;    // harmonic integrals skipped as below an ulp of the sum / -
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
@@ -746,7 +748,8 @@ struct AlbajarWork {
 template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
                                 double inv_sqNp, double N_perp, double omega_bar,
-                                double Axz, double ea, double e3, AlbajarWork *work, int sub = 0) {
+                                double Axz, double ea, double e3, AlbajarWork *work, int sub = 0,
+                                double dom = 0.0) {
     constexpr double md = (double)M, inv_md = 1.0 / md;
     HarmConst c;
     c.r2m1 = r * r - 1.0;
@@ -794,6 +797,36 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     if (zero) {
         if (work) work->n_zero++;
         return -mu * Pm * Pm * 0.0 * sq_r;
+    }
+    // Negligible next to the harmonics already summed (dom = their sum so far,
+    // abs_albajar_fast_body adds this one to it next): when a rigorous bound B
+    // on |this integral| is below 2^-58 |dom|, dom + h rounds to dom exactly
+    // (|h| < ulp(dom) / 4 with a 16x margin for B's own rounding and the node
+    // loop's ~1e-13), so the node loop is skipped and alpha is bit-identical.
+    // Far below the resonance of a higher harmonic its Maxwellian factor
+    // exp(mu (1 - gamma)) is e^-40 .. e^-760 of the lower one's: most third-
+    // harmonic integrals beside a second one.  B: |J_nu(x)| <= (x/2)^nu / nu!
+    // bounds |S_m|, |S_{m+1}|, |S_{m-1}| by 1/nu!; with h <= hx, |t| <= 1,
+    // every node's E <= E_max = exp(mu (1 - gamma_min)) and sum_i w_i = 2,
+    // |node sum| <= 4 E_max hx^(2m-1) (Pmax + Qmax).  The level ballot above
+    // already counted this lane, so the other lanes' polynomials do not change.
+    if (gl.negl_skip && dom != 0.0 && fabs(dom) < INFINITY && fabs(dom) > 1e-290) {
+        constexpr double iS = inv_fact(M), iS1 = inv_fact(M + 1), iSl = inv_fact(M - 1);
+        const double hx = c.hx, hx2 = hx * hx;
+        const double A = hx * (iS * iS), T1 = hx2 * iS1;
+        const double Bv = fabs(c.K2) * iSl * hx * T1, Cc = iS * (iSl + T1);
+        const double Pmax = A * (fabs(c.K0) + fabs(c.K3)) + Cc * fabs(c.K1) + Bv;
+        const double Qmax = A * fabs(c.K4) + Cc * fabs(c.K5);
+        double p = hx;  // hx^(2m-1)
+#pragma unroll
+        for (int k = 1; k < 2 * M - 1; k++) p *= hx;
+        const double R = (4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax)) * rcp_nz(fabs(dom));
+        const double Emax = exp_fast(mu * (1.0 - sqrt_nn(qmin)));
+        // R < 1e300: an E_max that underflowed to 0 cannot hide a huge R
+        if (R < 1e300 && R * Emax < 0x1p-58) {
+            if (work) work->n_negl++;
+            return 0.0;
+        }
     }
     if (work) {
         constexpr int kTerms[5] = {series_terms(0), series_terms(1), series_terms(2), series_terms(3),
@@ -904,11 +937,12 @@ TORJ_HD AlbPro albajar_prologue(double X, double Y, double N_abs, double N_par, 
 // harmonic, as the reference's `m < m_0` test makes it)
 template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double albajar_pro_harmonic(const GLTable &gl, const AlbPro &q, double N_par,
-                                    AlbajarWork *work, int sub = 0) {
-    const uint32_t z0 = work ? work->n_zero : 0u;
+                                    AlbajarWork *work, int sub = 0, double dom = 0.0) {
+    const uint32_t z0 = work ? work->n_zero + work->n_negl : 0u;
     const double h = albajar_harmonic<M, LPR, U>(gl, q.mu, (double)M * q.inv_m0, N_par, q.inv_sqNp,
-                                                 q.N_perp, q.omega_bar, q.Axz, q.ea, q.e3, work, sub);
-    if (work && work->n_zero == z0) work->n_harm++;
+                                                 q.N_perp, q.omega_bar, q.Axz, q.ea, q.e3, work, sub,
+                                                 dom);
+    if (work && work->n_zero + work->n_negl == z0) work->n_harm++;
     return h;
 }
 
@@ -931,7 +965,7 @@ TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, 
     if (work) work->n_active++;
     double c_abs = 0.0;
     if (!(2.0 < q.m_0)) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, N_par, work, sub);
-    if (!(3.0 < q.m_0)) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, N_par, work, sub);
+    if (!(3.0 < q.m_0)) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, N_par, work, sub, c_abs);
     return albajar_finish(q, c_abs, X, omega);
 }
 // the fused trace kernels' call (out of line there, see TORJ_ALB_ATTR); kernels
