@@ -327,7 +327,8 @@ def main():
                 {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
                  "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
                  "bessel_series_terms": int(cnt[4]),
-                 "harmonic_integrals_exact_zero": int(cnt[5])}),
+                 "harmonic_integrals_exact_zero": int(cnt[5]),
+                 "harmonic_integrals_negligible": int(cnt[6])}),
         }
         if world == 1 and not args.no_host_api:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,

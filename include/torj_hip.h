@@ -35,7 +35,7 @@ extern "C" {
 #endif
 
 #define TORJ_ABI_VERSION 5  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
-                               5: torj_trace_beam_device */
+                               5: torj_trace_beam_device, torj_power_deposition_profile */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -323,6 +323,22 @@ int torj_trace_check(torj_plasma_t p, void *stream);
  * processing milliseconds, then clears. */
 int torj_timing(torj_plasma_t p, int enable);
 int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post_ms);
+
+/* power_deposition_profile(plasma, s, x, dP_ds, psi_dP_dV) (src/plasma.jl:91-151)
+ * on the GPU for n_rays rays at once: ray r has n_points[r] >= 4 points with
+ * strictly increasing s, concatenated ray after ray -- s and dP_ds (sum of
+ * n_points), x component-major 3 x (sum of n_points).  psi at each point from
+ * the plasma's psi spline; the not-a-knot cubic fits of psi(s) - psi_j and
+ * dP/ds (Dierckx.Spline1D k = 3), their roots (Dierckx.roots, maxn = 8: the
+ * first 8 per boundary in s order), the |integral| per root pair and the
+ * outside-in walk, as torj_trace_ex's deposition = 1 applies to a trace.
+ * Outputs: dP_dV n_rays x n_psi, row r = ray r's dP_dV (its last entry 0, as
+ * the reference's), and P (n_rays).  Host pointers, synchronous.  Errors
+ * mirror the reference's: too few points or non-increasing s (Dierckx), a
+ * non-increasing psi_dP_dV. */
+int torj_power_deposition_profile(torj_plasma_t p, int n_rays, const int *n_points, const double *s,
+                                  const double *x, const double *dP_ds, int n_psi,
+                                  const double *psi_dP_dV, double *dP_dV, double *P);
 
 /* shell volumes dV[j] = V(psi_grid[j+1]) - V(psi_grid[j]), j < n_psi-1 (host;
  * src/plasma.jl:117-122) */

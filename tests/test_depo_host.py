@@ -79,3 +79,51 @@ def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode, grid_kind
     for nc in (1, 4):
         d2, k2, P2 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], nc)
         assert np.array_equal(k2, kstar) and np.array_equal(P2, P) and np.array_equal(d2, dPs)
+
+
+@pytest.mark.parametrize("periods", [3, 7])
+def test_host_deposition_root_cap_maxn_8(H, oplasma, periods):
+    """Dierckx.roots' maxn = 8 (src/plasma.jl:108,118; FITPACK sproot with
+    mest = 8): a ray whose psi(s) oscillates across the same surfaces keeps only
+    the first 8 roots of each boundary in s order.  Synthetic make_ray vectors
+    (psi(s) = 0.5 + 0.03 sin, periods full oscillations over the path) through
+    the product's fit (host build) against scipy's FITPACK restatement with
+    mest = 8 -- and, for 7 periods (14 roots per boundary), not equal to the
+    uncapped profile, so the cap is what is being checked."""
+    import warnings
+
+    import deposition_ref as D
+
+    n_steps, ds, s0 = 3000, 1e-4, 0.05
+    grid = np.linspace(0, 1, 250)
+    s = s0 + ds * np.arange(n_steps + 1)
+    u = (s - s0) / (n_steps * ds)
+    # in from the edge (launch point outside, psi = 1 at entry) to psi = 0.5 over
+    # the first 30 % of the path, then oscillating about it
+    v = np.clip((u - 0.3) / 0.7, 0.0, 1.0)
+    psi = np.where(u < 0.3, 1.0 - (0.5 / 0.3) * u, 0.5) + 0.03 * np.sin(2 * np.pi * periods * v) \
+        + 0.002 * u
+    dpds = np.exp(-((u - 0.45) / 0.3) ** 2) * (1.0 + 0.2 * np.cos(5 * u))
+    dpds[0] = 0.0  # make_ray's dP/ds is 0 at the entry point
+    psiL = 1.2
+    smp = np.stack([psi, dpds, s], axis=1)[None]  # (1, n_steps + 1, 3)
+    dPs, kstar, P = _run(H, n_steps, grid, np.array([s0]), np.array([n_steps]), np.array([psiL]),
+                         smp, 2, ds)
+    sv = np.concatenate([[0.0], s])
+    psi_v = np.concatenate([[psiL], psi])
+    dp_v = np.concatenate([[0.0], dpds])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # scipy: "The number of zeros exceeds mest"
+        prof8, P8 = D.power_deposition_profile(sv, psi_v, dp_v, grid, oplasma.volume, maxn=8)
+        prof_all, P_all = D.power_deposition_profile(sv, psi_v, dp_v, grid, oplasma.volume, maxn=1000)
+    dV = np.diff([oplasma.volume(p) for p in grid])
+    keep = np.arange(len(grid) - 1) > kstar[0]
+    shell = np.where(keep, dPs[:, 0], 0.0)
+    ref = prof8[:-1] * dV
+    assert np.abs(shell - ref).max() <= 1e-11 * np.abs(ref).max()
+    assert abs(P[0] - P8) <= 1e-11 * P8
+    if periods == 7:
+        assert abs(P_all - P8) > 1e-3 * P8  # the cap changes the reference's answer
+    # open-shell spill path under the capped walk
+    d1, k1, P1 = _run(H, n_steps, grid, np.array([s0]), np.array([n_steps]), np.array([psiL]), smp, 1, ds)
+    assert np.array_equal(d1, dPs) and np.array_equal(k1, kstar) and np.array_equal(P1, P)

@@ -186,3 +186,84 @@ def test_reference_deposition_in_ray_batches(gpu, T, hplasma):
         assert np.array_equal(getattr(a, f), getattr(b, f)), f
     assert np.array_equal(a.traj, b.traj, equal_nan=True)
     assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
+
+
+def _oscillating_ray(periods, n=3001, s0=0.05, ds=1e-4, R0=1.7, a=0.6):
+    """make_ray-style vectors of a synthetic path in the midplane whose psi goes
+    from outside the plasma in to 0.5 and then oscillates about it (the
+    circular equilibrium's psi_norm ~ ((R - R0)^2 + Z^2) / a^2)."""
+    s = np.concatenate([[0.0], s0 + ds * np.arange(n)])
+    u = (s[1:] - s0) / (ds * (n - 1))
+    v = np.clip((u - 0.3) / 0.7, 0.0, 1.0)
+    target = np.where(u < 0.3, 1.0 - (0.5 / 0.3) * u, 0.5) + 0.03 * np.sin(2 * np.pi * periods * v)
+    target = np.concatenate([[1.2], target])
+    R = R0 + a * np.sqrt(target)
+    x = np.stack([R, np.zeros_like(R), np.zeros_like(R)], axis=1)
+    uu = np.concatenate([[0.0], u])
+    dpds = np.exp(-((uu - 0.45) / 0.3) ** 2) * (1.0 + 0.2 * np.cos(5 * uu))
+    dpds[:2] = 0.0
+    return s, x, dpds
+
+
+@pytest.mark.parametrize("periods", [3, 7])
+def test_power_deposition_profile_entry_root_cap(gpu, T, hplasma, oplasma, periods):
+    """torj_power_deposition_profile (src/plasma.jl:91-151 as an entry point) on
+    a synthetic ray whose psi(s) oscillates across the same surfaces: with 7
+    oscillations each boundary near psi = 0.5 has 15 roots and Dierckx.roots'
+    maxn = 8 keeps the first 8 in s order.  dP_dV and P vs scipy's FITPACK
+    restatement with mest = 8, 1e-10 of the profile maximum; the uncapped
+    profile differs (so the cap is what is checked)."""
+    import warnings
+
+    import deposition_ref as D
+
+    s, x, dpds = _oscillating_ray(periods)
+    grid = np.linspace(0, 1, 250)
+    dP_dV, P = T.power_deposition_profile(hplasma, s, x, dpds, grid)
+    psi = np.array([oplasma.evaluate("psi", p) for p in x])
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")  # scipy: "The number of zeros exceeds mest"
+        ref, P_ref = D.power_deposition_profile(s, psi, dpds, grid, oplasma.volume, maxn=8)
+        _, P_all = D.power_deposition_profile(s, psi, dpds, grid, oplasma.volume, maxn=1000)
+    assert np.abs(dP_dV - ref).max() <= 1e-10 * np.abs(ref).max()
+    assert abs(P - P_ref) <= 1e-10 * P_ref and dP_dV[-1] == 0.0
+    if periods == 7:
+        assert abs(P_all - P_ref) > 1e-3 * P_ref
+
+
+def test_power_deposition_profile_entry_on_rays(gpu, T, hplasma, oplasma, fan_states):
+    """The entry point on make_ray's own vectors of traced rays (several rays in
+    one call) vs the FITPACK restatement, and the reference's input errors."""
+    import deposition_ref as D
+    from torj_hip import synthetic as S
+
+    s_ = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(s_["steering_angle_pol"], s_["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s_["R0"], 0.0, s_["z0"]], N0, s_["spot_size"],
+                                            s_["inverse_curvature_radius"], s_["f_abs_test"],
+                                            N_rings=3, min_azimuthal_points=5)
+    om = 2 * np.pi * s_["f_abs_test"]
+    xp, Np, s0, st = T.ray_entry(hplasma, pos, dirs, om, 1)
+    idx = np.arange(0, len(w), 5)
+    grid = np.linspace(0, 1, 400)
+    o = oplasma.trace(xp[idx], Np[idx], om, 1, 1e-4, 2000, samples=True, s0=s0[idx], traj_stride=1)
+    ss, xs, ds_, refs = [], [], [], []
+    for k, i in enumerate(idx):
+        m = int(o["steps"][k])
+        sv, psi, dpds = D.ray_vectors(pos[i], s0[i], 1e-4, m, o["samples"][k],
+                                      oplasma.evaluate("psi", pos[i]))
+        xv = np.vstack([pos[i][None], xp[i][None], o["traj"][k, :m, :3]])
+        psi_x = np.array([oplasma.evaluate("psi", p) for p in xv])
+        ss.append(sv), xs.append(xv), ds_.append(dpds)
+        refs.append(D.power_deposition_profile(sv, psi_x, dpds, grid, oplasma.volume))
+    dP_dV, P = T.power_deposition_profile(hplasma, ss, xs, ds_, grid)
+    for k in range(len(idx)):
+        ref, P_ref = refs[k]
+        assert np.abs(dP_dV[k] - ref).max() <= 1e-10 * max(np.abs(ref).max(), 1e-300)
+        assert abs(P[k] - P_ref) <= 1e-10 * max(P_ref, 1e-300)
+    with pytest.raises(T.TorjError, match="need >= 4"):
+        T.power_deposition_profile(hplasma, ss[0][:3], xs[0][:3], ds_[0][:3], grid)
+    bad = ss[0].copy()
+    bad[5] = bad[4]
+    with pytest.raises(T.TorjError, match="strictly increasing"):
+        T.power_deposition_profile(hplasma, bad, xs[0], ds_[0], grid)

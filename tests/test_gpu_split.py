@@ -222,3 +222,67 @@ def test_split_serial_equals_overlapped(gpu, T, hplasma, deposition):
         assert np.array_equal(a.dP_shell, b.dP_shell)
     else:  # binned: fp64 atomics, order-dependent in the last bits
         assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
+
+
+def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
+    """The skip of provably negligible harmonic integrals (torj_math.hpp
+    albajar_harmonic: bound below 2^-58 of the harmonics already summed) leaves
+    every output bit-identical: TORJ_NEGL_SKIP=0 (re-read by abs_Al_init, which
+    re-uploads the GL table) against the default, on the split pipeline (the
+    default for large beams) and the fused one-lane kernel; the skip fires
+    (work counter [6]) and moves its integrals out of counter [3]."""
+    import ctypes
+    import os
+
+    import torch
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    n = len(w)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, psi_grid=np.linspace(0, 1, 1000),
+              deposition="reference", x_launch=pos, s0=s0)
+    dev = torch.device("cuda", 0)
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    x0, N0 = t(xp.T), t(Np.T)
+
+    def counters(sched):
+        state = torch.empty((7, n), dtype=torch.float64, device=dev)
+        st = torch.empty(n, dtype=torch.int32, device=dev)
+        k = torch.empty(n, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+        cfg = T._lib.TraceCfg(om, 1, 1e-4, 2000, 20, 1.0, 1e-6, 1, 0)
+        stream = torch.cuda.current_stream(dev)
+        hplasma.set_sched(sched, 0)
+        try:
+            T._lib.check(T.lib().torj_trace_device(hplasma.handle, cfg, n, x0.data_ptr(), N0.data_ptr(),
+                                                   None, 0, None, state.data_ptr(), st.data_ptr(),
+                                                   k.data_ptr(), None, None, None,
+                                                   ctypes.c_void_p(cnt.data_ptr()), stream.cuda_stream))
+            T._lib.check(T.lib().torj_trace_check(hplasma.handle, stream.cuda_stream))
+        finally:
+            hplasma.set_sched(-1)
+        return cnt.cpu().numpy()
+
+    res, cnts = {}, {}
+    old = os.environ.get("TORJ_NEGL_SKIP")
+    try:
+        for skip in ("0", "1"):
+            os.environ["TORJ_NEGL_SKIP"] = skip
+            T.abs_Al_init(24)
+            for sched in (3, 0):
+                res[skip, sched] = _run(T, hplasma, sched, 0, xp, Np, om, 1, **kw)
+                cnts[skip, sched] = counters(sched)
+    finally:
+        if old is None:
+            os.environ.pop("TORJ_NEGL_SKIP", None)
+        else:
+            os.environ["TORJ_NEGL_SKIP"] = old
+        T.abs_Al_init(24)
+    for sched in (3, 0):
+        a, b = res["0", sched], res["1", sched]
+        for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+            assert np.array_equal(getattr(a, f), getattr(b, f)), (sched, f)
+        assert np.array_equal(a.traj, b.traj, equal_nan=True)
+        c0, c1 = cnts["0", sched], cnts["1", sched]
+        assert c0[6] == 0 and c1[6] > 0.1 * c0[3], (c0, c1)
+        assert c1[3] + c1[6] == c0[3] and np.array_equal(c0[[0, 1, 2, 5]], c1[[0, 1, 2, 5]])
+    assert np.array_equal(cnts["1", 3], cnts["1", 0])

@@ -135,3 +135,70 @@ def test_albajar_host_build_matches_golden(H):
         assert (np.abs(out[big] - want[big]) / np.abs(want[big])).max() < 1e-10
         small = ~nan & ~zero & ~big
         assert np.abs(out[small] - want[small]).max() < 1e-20
+
+
+def _stage_points(n_rays=24, every=50):
+    """(omega, X, Y, |N|, N_par, Te) at states along rays of the headline fan
+    (92.5 GHz X-mode, oracle RK4): the inputs abs_Albajar_fast sees in a trace."""
+    import oracle as O
+    from torj_hip import synthetic as S
+    import torj_hip as T
+
+    O.abs_al_init(24)
+    eq = S.circular_tokamak()
+    OP = O.OraclePlasma(*S.plasma_args(eq))
+    s = S.SETUP
+    f = s["f_abs_test"]
+    om = 2 * np.pi * f
+    N0 = O.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = O.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=92,
+                                            min_azimuthal_points=11)
+    idx = np.linspace(0, len(w) - 1, n_rays).astype(int)
+    P = T.Plasma(*S.plasma_args(eq))
+    xp, Np, s0, st = T.ray_entry(P, pos[idx], dirs[idx], om, 1)
+    rows = []
+    for k in range(every, 2001, every):
+        r = OP.trace(xp, Np, om, 1, 1e-4, k)
+        for i in range(len(idx)):
+            x, N = r["state"][i, :3], r["state"][i, 3:6]
+            X, Y, Npar, _ = OP.eval_plasma(x, N, om)
+            rows.append((om, X, Y, np.linalg.norm(N), Npar, OP.T_e(x)))
+    return np.array(rows)
+
+
+def test_albajar_negligible_harmonic_skip_is_bit_identical(H):
+    """The skip of a harmonic integral whose rigorous bound is below 2^-58 of
+    the harmonics already summed (torj_math.hpp albajar_harmonic) leaves
+    abs_Albajar_fast bit-identical: host build with the skip on and off over
+    stage points along rays of the headline fan (where the third harmonic is
+    summed beside the second) and the oracle's golden sweep; the skip fires."""
+    import json
+
+    rows = _stage_points()
+    d = json.load(open(os.path.join(HERE, "golden", "albajar.json")))
+    g = np.array(d["rows"], dtype=float)
+    H.wh_albajar.argtypes = [C.c_int] + [_dp] * 6 + [C.c_int, _dp, _dp, C.c_int, _dp]
+    H.wh_albajar_work.argtypes = [C.c_int] + [_dp] * 6 + [C.c_int, C.POINTER(C.c_uint)]
+    H.wh_set_negl_skip.argtypes = [C.c_int]
+    t, w = np.polynomial.legendre.leggauss(24)
+    skipped = 0
+    for pts, mode in ((rows, 1), (g[g[:, 6] == 1][:, :6], 1), (g[g[:, 6] == -1][:, :6], -1)):
+        n = len(pts)
+        cols = [np.ascontiguousarray(pts[:, k]) for k in range(6)]
+        out = {}
+        for on in (1, 0):
+            a = np.zeros(n)
+            H.wh_albajar(n, *[_d(c) for c in cols], mode, _d(t), _d(w), 24, _d(a))  # sets up the table
+            H.wh_set_negl_skip(on)
+            H.wh_albajar(n, *[_d(c) for c in cols], mode, _d(t), _d(w), 24, _d(a))
+            wk = np.zeros(3 * n, dtype=np.uint32)
+            H.wh_albajar_work(n, *[_d(c) for c in cols], mode, wk.ctypes.data_as(C.POINTER(C.c_uint)))
+            out[on] = (a, wk.reshape(-1, 3))
+        assert np.array_equal(out[1][0].view(np.int64), out[0][0].view(np.int64))
+        assert out[0][1][:, 2].sum() == 0
+        # every skipped integral is one the no-skip run evaluated
+        assert out[1][1][:, 0].sum() + out[1][1][:, 2].sum() == out[0][1][:, 0].sum()
+        skipped += int(out[1][1][:, 2].sum())
+    H.wh_set_negl_skip(1)
+    assert skipped > 0.2 * len(rows)

@@ -63,6 +63,10 @@ struct FitArgs {
     int *kstar;                        // n: break shell
     double *dP;                        // n_psi + 1 (weighted sums; written by k_shell_sum)
     double *Pray;                      // n: per-ray deposited power (reference's P)
+    // torj_power_deposition_profile (caller-given vectors): points per ray; every
+    // point j of ray i (s, psi, dP/ds) is then row j of smp_s / smp_psi /
+    // smp_dpds, launch and entry points included.  Null for a trace's samples.
+    const int *npts;
 };
 
 TORJ_HD int imin(int x, int y) { return x < y ? x : y; }
@@ -78,12 +82,19 @@ struct RayData {
     // arc length of point j: 0 (launch), s0 (entry), s0 + (j-1) ds for RK4 (the
     // fma the trajectory output uses), else the integrator's stored s
     TORJ_HD double S(int j) const {
+        if (a->npts) return a->smp_s[smp_at(j, i, a->rows)];
         if (j == 0) return 0.0;
         return a->s_uniform ? fma((double)(j - 1), a->ds, s0) : a->smp_s[smp_at(j - 1, i, a->rows)];
     }
-    TORJ_HD double h(int j) const { return j == 0 ? s0 : S(j + 1) - S(j); }
-    TORJ_HD double Ypsi(int j) const { return j == 0 ? psiL : a->smp_psi[smp_at(j - 1, i, a->rows)]; }
-    TORJ_HD double YP(int j) const { return j <= 1 ? 0.0 : a->smp_dpds[smp_at(j - 1, i, a->rows)]; }
+    TORJ_HD double h(int j) const { return (j == 0 && !a->npts) ? s0 : S(j + 1) - S(j); }
+    TORJ_HD double Ypsi(int j) const {
+        if (a->npts) return a->smp_psi[smp_at(j, i, a->rows)];
+        return j == 0 ? psiL : a->smp_psi[smp_at(j - 1, i, a->rows)];
+    }
+    TORJ_HD double YP(int j) const {
+        if (a->npts) return a->smp_dpds[smp_at(j, i, a->rows)];
+        return j <= 1 ? 0.0 : a->smp_dpds[smp_at(j - 1, i, a->rows)];
+    }
     TORJ_HD double &EE(int j) const { return a->E[smp_at(j, i, a->rows)]; }
     TORJ_HD double &GPSI(int j) const { return a->Gpsi[smp_at(j, i, a->rows)]; }
     TORJ_HD double &GPP(int j) const { return a->GP[smp_at(j, i, a->rows)]; }
@@ -224,7 +235,16 @@ TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, double
 //    the lane's own element.
 constexpr int kOpenCache = 2;
 
-template <int NC = kOpenCache>
+// Dierckx.roots(spline; maxn = 8) (the reference's call, src/plasma.jl:108,118,
+// default maxn of Dierckx.jl 0.5.4): FITPACK sproot with mest = 8 keeps the
+// first 8 zeros of each boundary's spline in s order (scipy's sproot, the
+// oracle's restatement, does the same and warns).  A boundary can have more
+// than 8 roots only if psi(s) has more than 8 monotone runs (one root per
+// boundary per run), so the walk counts its runs and re-walks the rare ray
+// with more in the capped mode below (exact per-boundary counts in memory).
+constexpr int kMaxRoots = 8;
+
+template <int NC = kOpenCache, bool CAP = false>
 struct Walker {
     const FitArgs *a;
     int i;
@@ -234,11 +254,16 @@ struct Walker {
     double oF[NC];  // F at their opening root
     bool spilled;           // some open shell lives in Fopen
     int run_k0, run_k1, run_d;  // current run of roots (run_d = 0: none)
+    int runs, last_d;       // monotone runs of psi(s) so far, direction of the last one
     TORJ_HD void init() {
 #pragma unroll
         for (int u = 0; u < NC; u++) oq[u] = -1, oF[u] = 0.0;
         spilled = false;
         run_d = 0, run_k0 = run_k1 = 0;
+        runs = 0, last_d = 0;
+    }
+    TORJ_HD void piece(int d) {  // a monotone piece of direction d (+1 / -1) of psi(s)
+        if (d != last_d) runs++, last_d = d;
     }
     TORJ_HD void cadd(int k, int v) {
         __hip_atomic_fetch_add(a->cnt + (size_t)k * a->n + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -283,7 +308,11 @@ struct Walker {
     // levels are crossed in direction d (+1 upwards, -1 downwards): count it and
     // toggle the shells it bounds (k-1 above it, k below it)
     TORJ_HD void root(int k, double Fr, int d) {
-        if (d == run_d && k == run_k1 + d) {
+        if constexpr (CAP) {  // direct count of boundary k's roots so far: the 9th is dropped
+            int &c = a->cnt[(size_t)k * a->n + i];
+            if (c >= kMaxRoots) return;
+            c++;
+        } else if (d == run_d && k == run_k1 + d) {
             run_k1 = k;
         } else {
             flush_run();
@@ -346,11 +375,13 @@ TORJ_HD void walk_segment(W_ &W, const Cubic &qs, double y1, const Cubic &qP, bo
         int k, kend, d;
         if (fb > fa) {  // increasing: boundaries fa < L <= fb (fa <= L at s = 0), ascending
             d = 1;
+            W.piece(1);
             k = first0 ? level_above(a, fa, false) : W.cur.c;
             W.cur.seek(fb);
             kend = W.cur.c;
         } else if (fb < fa) {  // decreasing: boundaries fb <= L < fa (<= fa at s = 0), descending
             d = -1;
+            W.piece(-1);
             k = (first0 ? level_above(a, fa, true) : W.cur.c - (fa == W.cur.lo)) - 1;
             W.cur.seek(fb);
             kend = W.cur.c - (fb == W.cur.lo) - 1;  // #boundaries < fb, minus one
@@ -427,13 +458,14 @@ TORJ_HD void walk_ray(W_ &W, const RayData &R) {
 // shell k* and the ray's deposited power P.  psiL = psi at the launch point.
 template <int NC>
 TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
-    const int m = a.steps[i] + 2;  // launch point, entry point, one per step
-    if (m < 4 || !(a.s0[i] > 0.0)) {  // FITPACK needs > k = 3 strictly increasing points
+    // a trace: launch point, entry point, one per step; or the caller's points
+    const int m = a.npts ? a.npts[i] : a.steps[i] + 2;
+    if (m < 4 || (!a.npts && !(a.s0[i] > 0.0))) {  // FITPACK needs > k = 3 strictly increasing points
         a.kstar[i] = a.n_psi;  // no shell counts
         a.Pray[i] = 0.0;
         return;
     }
-    RayData R{&a, i, m, a.s0[i], psiL};
+    RayData R{&a, i, m, a.npts ? 0.0 : a.s0[i], psiL};
     nak_eliminate(R);
     Walker<NC> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
     W.init();
@@ -445,25 +477,45 @@ TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+    const size_t n = a.n;
+    const int L = a.n_psi;
+    const bool capped = W.runs > kMaxRoots;
+    if (capped) {  // some boundary may have > maxn roots: redo the ray with the cap
+        for (int k = 0; k <= L; k++) a.cnt[(size_t)k * n + i] = 0;
+        for (int q = 0; q + 1 < L; q++) {
+            a.dPs[(size_t)q * n + i] = 0.0;
+            a.Fopen[(size_t)q * n + i] = NAN;
+        }
+#ifdef __HIP_DEVICE_COMPILE__
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        Walker<NC, true> Wc{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+        Wc.init();
+        walk_ray(Wc, R);
+#ifdef __HIP_DEVICE_COMPILE__
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    }
     // the reference's outside-in walk stops at the first shell whose two
     // boundaries have < 2 roots together (src/plasma.jl:120-124)
     // root counts: cnt[k] = sum_{j <= k} cdiff[j] = -sum_{j > k} cdiff[j] (the
-    // differences sum to zero), accumulated from the top
+    // differences sum to zero), accumulated from the top; the capped walk
+    // stores the counts themselves
     int kstar = -1;
-    const size_t n = a.n;
-    const int L = a.n_psi;
     int suf = a.cnt[(size_t)L * n + i];  // sum_{j > L-1} cdiff[j]
-    int c_up = -suf;                      // cnt[L-1]
+    int c_up = capped ? a.cnt[(size_t)(L - 1) * n + i] : -suf;  // cnt[L-1]
     for (int k0 = L - 2; k0 >= 0 && kstar < 0; k0 -= kChunk) {
         int dv[kChunk];
 #pragma unroll
-        for (int u = 0; u < kChunk; u++) dv[u] = a.cnt[(size_t)imax(k0 - u + 1, 0) * n + i];
+        for (int u = 0; u < kChunk; u++) dv[u] = a.cnt[(size_t)imax(k0 - u + (capped ? 0 : 1), 0) * n + i];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {  // shell k = k0 - u: boundaries k and k + 1
             const int k = k0 - u;
             if (k >= 0 && kstar < 0) {
                 suf += dv[u];  // now sum_{j > k}
-                const int c_k = -suf;
+                const int c_k = capped ? dv[u] : -suf;
                 if (c_up + c_k < 2) kstar = k;
                 c_up = c_k;
             }

@@ -1388,6 +1388,34 @@ __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
     fit_depo_ray<kOpenCache>(a, i, psi_at(a.coef, a.g, xl));
 }
+// torj_power_deposition_profile: the caller's vectors of ray i (points off[i] ..
+// off[i] + npts[i] - 1) into the fit's per-point rows, psi(s_j) from the psi
+// spline at x_j (src/plasma.jl:95-98: psi_norm_spline(hypot(x, y), z))
+__global__ void __launch_bounds__(64) k_profile_samples(FitArgs a, const long *off, const double *s,
+                                                        const double *x, size_t n_all, const double *dpds) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    for (int j = 0; j < a.npts[i]; j++) {
+        const size_t q = (size_t)off[i] + j;
+        const double xq[3] = {x[q], x[n_all + q], x[2 * n_all + q]};
+        const size_t o = smp_at(j, i, a.rows);
+        // (FitArgs holds the sample rows read-only for the fit; this kernel fills them)
+        const_cast<double *>(a.smp_psi)[o] = psi_at(a.coef, a.g, xq);
+        const_cast<double *>(a.smp_dpds)[o] = dpds[q];
+        const_cast<double *>(a.smp_s)[o] = s[q];
+    }
+}
+__global__ void __launch_bounds__(64, 2) k_fit_profile(FitArgs a) {
+    extern __shared__ double s_grid[];
+    if (a.n_psi <= kFitGridLds) {
+        for (int k = threadIdx.x; k < a.n_psi; k += 64) s_grid[k] = a.grid[k];
+        __syncthreads();
+        a.grid = s_grid;
+    }
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    fit_depo_ray<kOpenCache>(a, i, 0.0);
+}
 // a work-queue launch's outcome into the handle's sticky flags (bit 1 stall
 // watchdog, bit 2 not every group retired); read by torj_trace_check
 __global__ void k_sched_fold(const SchedCtl *ctl, unsigned G, int *flags) {
@@ -2919,6 +2947,90 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
 }
 
 extern "C" {
+
+int torj_power_deposition_profile(torj_plasma_t p, int n_rays, const int *n_points, const double *s,
+                                  const double *x, const double *dP_ds, int n_psi,
+                                  const double *grid, double *dP_dV, double *P) {
+    if (!p) return fail("bad plasma handle");
+    if (n_rays < 0 || n_psi < 2 || !grid) return fail("power_deposition_profile: n_rays >= 0, n_psi >= 2 needed");
+    if (n_rays == 0) return 0;
+    if (!n_points || !s || !x || !dP_ds || !dP_dV || !P) return fail("power_deposition_profile: null argument");
+    for (int k = 1; k < n_psi; k++)
+        if (!(grid[k] > grid[k - 1])) return fail("psi_dP_dV must be strictly increasing");
+    std::vector<long> off(n_rays);
+    long tot = 0;
+    int rows = 0;
+    for (int r = 0; r < n_rays; r++) {
+        // Dierckx.Spline1D(s, y, k = 3) needs m > k points with strictly
+        // increasing s (FITPACK curfit's input check)
+        if (n_points[r] < 4) return fail("power_deposition_profile: ray %d has %d points (need >= 4)", r, n_points[r]);
+        for (int j = 1; j < n_points[r]; j++)
+            if (!(s[tot + j] > s[tot + j - 1]))
+                return fail("power_deposition_profile: s must be strictly increasing (ray %d, point %d)", r, j);
+        off[r] = tot;
+        tot += n_points[r];
+        rows = std::max(rows, n_points[r]);
+    }
+    if (ensure_device(p)) return -1;
+    hipStream_t st = p->stream;
+    const size_t N = (size_t)n_rays, L = (size_t)n_psi, K = (size_t)rows, KN = smp_elems(N, K);
+    DevBufs B;
+    double *d_s, *d_x, *d_dp, *d_grid, *d_smp, *d_Pr;
+    int *d_np, *d_kstar, *d_cnt;
+    long *d_off;
+    if (dupload(&d_s, s, (size_t)tot, st) || dupload(&d_x, x, 3 * (size_t)tot, st) ||
+        dupload(&d_dp, dP_ds, (size_t)tot, st) || dupload(&d_grid, grid, L, st) ||
+        dupload(&d_np, n_points, N, st) || dupload(&d_off, off.data(), N, st) ||
+        dalloc(&d_smp, 6 * KN + 2 * L * N, true) || dalloc(&d_cnt, (L + 1) * N, true) ||
+        dalloc(&d_kstar, N, true) || dalloc(&d_Pr, N, true))
+        return -1;
+    B.track(d_s), B.track(d_x), B.track(d_dp), B.track(d_grid), B.track(d_np), B.track(d_off);
+    B.track(d_smp), B.track(d_cnt), B.track(d_kstar), B.track(d_Pr);
+    FitArgs fa{};
+    fa.coef = p->d_coef;
+    fa.g = p->g;
+    fa.n = n_rays;
+    fa.n_psi = n_psi;
+    fa.grid = d_grid;
+    fa.rows = K;
+    fa.npts = d_np;
+    fa.steps = d_np;
+    fa.smp_psi = d_smp;
+    fa.smp_dpds = d_smp + KN;
+    fa.smp_s = d_smp + 2 * KN;
+    fa.E = d_smp + 3 * KN;
+    fa.Gpsi = d_smp + 4 * KN;
+    fa.GP = d_smp + 5 * KN;
+    fa.Fopen = d_smp + 6 * KN;
+    fa.dPs = fa.Fopen + L * N;
+    fa.cnt = d_cnt;
+    fa.kstar = d_kstar;
+    fa.Pray = d_Pr;
+    HIPCK(hipMemsetAsync(fa.cnt, 0, (L + 1) * N * sizeof(int), st));
+    HIPCK(hipMemsetAsync(fa.Fopen, 0xFF, L * N * sizeof(double), st));  // NaN: every shell closed
+    HIPCK(hipMemsetAsync(fa.dPs, 0, L * N * sizeof(double), st));
+    hipLaunchKernelGGL(k_profile_samples, dim3(nblocks(n_rays, 64)), dim3(64), 0, st, fa, d_off, d_s, d_x,
+                       (size_t)tot, d_dp);
+    const size_t lds = n_psi <= kFitGridLds ? (size_t)n_psi * sizeof(double) : 0;
+    hipLaunchKernelGGL(k_fit_profile, dim3(nblocks(n_rays, 64)), dim3(64), lds, st, fa);
+    HIPCK(hipGetLastError());
+    std::vector<double> dPs(L * N);
+    std::vector<int> kstar(N);
+    if (ddownload(dPs.data(), fa.dPs, (L - 1) * N, st) || ddownload(kstar.data(), d_kstar, N, st) ||
+        ddownload(P, d_Pr, N, st))
+        return -1;
+    HIPCK(hipStreamSynchronize(st));
+    // dP_dV[j] = dP_j / (V(psi_{j+1}) - V(psi_j)) above the break shell, 0 below it
+    // and at the last boundary (src/plasma.jl:141)
+    std::vector<double> dV(L - 1);
+    torj_shell_volumes(p, n_psi, grid, dV.data());
+    for (size_t r = 0; r < N; r++) {
+        double *row = dP_dV + r * L;
+        for (size_t j = 0; j < L; j++)
+            row[j] = (j + 1 < L && (int)j > kstar[r]) ? dPs[j * N + r] / dV[j] : 0.0;
+    }
+    return 0;
+}
 
 int torj_timing(torj_plasma_t p, int enable) {
     if (!p) return fail("bad plasma handle");

@@ -149,6 +149,28 @@ function shell_volumes(p::GPUPlasma, g::Vector{Float64})
     return dV
 end
 
+"""power_deposition_profile -- same signature and return tuple as
+TorJ.power_deposition_profile (src/plasma.jl:91-151), on the GPU: psi at x from the
+plasma's spline, the not-a-knot fits, Dierckx.roots (maxn = 8) pairing and the
+outside-in walk.  Returns (dP_dV, P)."""
+function power_deposition_profile(p::GPUPlasma, s::Vector{Float64}, x::Vector{Vector{Float64}},
+                                  dP_ds::Vector{Float64}, psi_dP_dV::Vector{Float64})
+    n = length(s)
+    (length(x) == n && length(dP_ds) == n) || throw(DimensionMismatch("s, x, dP_ds lengths differ"))
+    xm = Matrix{Float64}(undef, n, 3)  # n x 3 column-major = the ABI's component-major 3 x n
+    for i in 1:n, c in 1:3
+        xm[i, c] = x[i][c]
+    end
+    dP_dV, P = zeros(length(psi_dP_dV)), zeros(1)
+    np = Cint[n]
+    check(ccall((:torj_power_deposition_profile, libtorj), Cint,
+                (Ptr{Cvoid}, Cint, Ptr{Cint}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Cint,
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                p.h, 1, np, s, xm, dP_ds, length(psi_dP_dV), psi_dP_dV, dP_dV, P))
+    return dP_dV, P[1]
+end
+power_deposition_profile(p::TorJ.Plasma, args...) = power_deposition_profile(gpu_plasma(p), args...)
+
 """make_ray -- same signature and return tuple as TorJ.make_ray (src/solve.jl:135-181)."""
 function make_ray(p::GPUPlasma, x0::AbstractVector, N_vacuum::AbstractVector, f::Real,
                   mode::Integer, s_max::Float64, psi_dP_dV::AbstractVector; ds::Float64=1e-4,

@@ -100,6 +100,8 @@ _SIGS = {
     "torj_trace_device_ex": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int] +
                              [C.c_void_p] * 3 + [C.c_int] + [C.c_void_p] * 11),
     "torj_shell_volumes": (C.c_int, [C.c_void_p, C.c_int, _dp, _dp]),
+    "torj_power_deposition_profile": (C.c_int, [C.c_void_p, C.c_int, _ip, _dp, _dp, _dp, C.c_int, _dp,
+                                                _dp, _dp]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -22,18 +22,25 @@ FLOPS_SERIES_TERM = 4       # per Horner term (two series, one fma each)
 FLOPS_STEP_OVERHEAD = 234   # RK4 combination, exp(-tau), psi evaluation
 FLOPS_ZERO_TEST = 12        # per harmonic found exactly zero: the gamma_min bound (its setup
                             # is FLOPS_HARM; the node loop it skips is not counted)
+FLOPS_NEGL_TEST = 59        # per harmonic skipped as below an ulp of the sum (torj_math.hpp
+                            # albajar_harmonic): the bound's Bessel/polarisation factors (33),
+                            # exp(mu (1 - gamma_min)) (26 + 3) -- on top of FLOPS_HARM and the
+                            # gamma_min test; the node loop it skips is not counted.  Tests that
+                            # do not skip cost the same and are not counted (conservative).
 
 
 def algorithmic_flops(counters, n_gl: int = 24) -> float:
     """counters = (ray_steps, rhs_evals, alpha_active, harmonic_integrals, series_terms
-    [, harmonic_integrals_exact_zero])."""
+    [, harmonic_integrals_exact_zero [, harmonic_integrals_negligible]])."""
     steps, rhs, act, harm, terms = (float(c) for c in counters[:5])
     zero = float(counters[5]) if len(counters) > 5 else 0.0
+    negl = float(counters[6]) if len(counters) > 6 else 0.0
     pairs = (n_gl + 1) // 2
     return (steps * FLOPS_STEP_OVERHEAD + rhs * FLOPS_RHS_COLD
             + act * (FLOPS_ALPHA_PRE + FLOPS_ALPHA_POST)
             + harm * (FLOPS_HARM + pairs * FLOPS_PAIR_SHARED + n_gl * FLOPS_NODE)
             + zero * (FLOPS_HARM + FLOPS_ZERO_TEST)
+            + negl * (FLOPS_HARM + FLOPS_ZERO_TEST + FLOPS_NEGL_TEST)
             + FLOPS_SERIES_TERM * (terms - harm * pairs))
 
 

@@ -149,3 +149,29 @@ def eval_plasma(plasma: Plasma, x, N, omega: float):
     if _single(x):
         return float(o[6, 0]), float(o[7, 0]), float(o[8, 0]), o[9:12, 0].copy()
     return o[6], o[7], o[8], o[9:12].T.copy()
+
+
+def power_deposition_profile(plasma, s, x, dP_ds, psi_dP_dV):
+    """power_deposition_profile(plasma, s, x, dP_ds, psi_dP_dV) (src/plasma.jl:91-151)
+    -> (dP_dV, P), on the GPU (torj_power_deposition_profile).  One ray: s (n,),
+    x (n, 3) or a list of 3-vectors, dP_ds (n,).  Several rays: lists of such
+    arrays -> (dP_dV (n_rays, n_psi), P (n_rays,))."""
+    batched = isinstance(s, (list, tuple)) and len(s) > 0 and np.ndim(s[0]) == 1
+    ss = [f64(v) for v in s] if batched else [f64(s)]
+    xs = [np.asarray(v, dtype=np.float64).reshape(-1, 3) for v in x] if batched else \
+        [np.asarray(x, dtype=np.float64).reshape(-1, 3)]
+    ds = [f64(v) for v in dP_ds] if batched else [f64(dP_ds)]
+    npts = np.array([len(v) for v in ss], dtype=np.int32)
+    for a, b, c in zip(ss, xs, ds):
+        if not (len(a) == len(b) == len(c)):
+            raise ValueError("s, x and dP_ds must have one entry per point")
+    s_all = np.ascontiguousarray(np.concatenate(ss))
+    x_all = soa(np.concatenate(xs))
+    d_all = np.ascontiguousarray(np.concatenate(ds))
+    g = f64(psi_dP_dV)
+    out = np.zeros((len(ss), len(g)))
+    P = np.zeros(len(ss))
+    check(lib().torj_power_deposition_profile(plasma.handle, len(ss), npts.ctypes.data_as(C.POINTER(C.c_int)),
+                                              dptr(s_all), dptr(x_all), dptr(d_all), len(g), dptr(g),
+                                              dptr(out), dptr(P)))
+    return (out, P) if batched else (out[0], float(P[0]))
