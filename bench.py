@@ -692,11 +692,38 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
                           f"relative, i.e. {1e-6 * {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10):g} "
                           f"absolute below tau = 1e-6 (the floor: P moves by < 1 ulp there); status "
                           f"and steps exact")}
-        if model == 2:
-            parity["note"] = ("weakly relativistic: tau accumulated at Te < 1 keV (cold-edge "
-                              "harmonic crossings) is conditioning-limited -- the fsup recurrence "
-                              "cancels, so TOMS 680 (oracle), Weideman (GPU) and scipy (warm_ref) "
-                              "restatements differ there at up to ~1e-2 (DESIGN.md 3.6)")
+        if warm:
+            # a-priori conditioning flag: how far each sampled ray's tau
+            # moves when every RK4 stage point's warm-alpha inputs move by 64 ulps
+            # (oracle or_warm_sensitivity, untimed, from the trajectory alone --
+            # independent of the GPU's answer); flagged when that exceeds half the bar
+            bar = {2: 1e-8, 3: 1e-9}[model]
+            t0 = time.perf_counter()
+            sens = OP.warm_sensitivity(xp[idx], Np[idx], omega, args.mode, args.ds, r["steps"],
+                                       iwarm=1 if model == 2 else 3, n_threads=threads)
+            t_sens = time.perf_counter() - t0
+            rel_sens = sens / np.maximum(np.abs(os_[:, 6]), 1e-6)
+            flagged = rel_sens > 0.5 * bar
+            ok = ~flagged
+            e_all = np.maximum(np.maximum(ex, eN), et)
+            parity["conditioning"] = {
+                "flag": "tau sensitivity to 64-ulp (2^-46 relative) perturbations of every stage "
+                        "point's alpha inputs (Y up / down, X N_par Te jointly) > bar / 2 (relative, "
+                        "tau floor 1e-6); oracle or_warm_sensitivity, a-priori",
+                "rays_flagged": int(flagged.sum()),
+                "rays_unflagged": int(ok.sum()),
+                "rays_within_bar_unflagged": int((e_all[ok] <= bar).sum()),
+                "max_rel_tau_unflagged": float(et[ok].max()) if ok.any() else None,
+                "p99_rel_tau_unflagged": float(np.quantile(et[ok], 0.99)) if ok.any() else None,
+                "rays_out_of_bar_flagged": int((e_all[flagged] > bar).sum()),
+                "seconds": t_sens,
+                "flagged_fan_indices": [int(i) for i in idx[flagged][:64]],
+            }
+            parity["note"] = ("warm model: flagged rays have an optical depth that no double-"
+                              "precision restatement determines to the bar (cold-edge harmonic "
+                              "crossings: fsup's recurrence cancels, and warmdisp's root selector "
+                              "is decided at the 1e-11 level, one ulp of Y picking the other root; "
+                              "50-digit evidence in profiles/r03/c5_conditioning_evidence.json)")
     what = ("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
             else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",

@@ -224,6 +224,21 @@ class OraclePlasma:
                           1.0 / self.grad_norm(x, N, omega, mode), mode,
                           1 if model == 2 else 3)[0]
 
+    def warm_sensitivity(self, x0, N0, omega, mode, ds, steps, iwarm=1, eta=2.0 ** -46,
+                         n_threads=None):
+        """or_warm_sensitivity: per ray, sum over its RK4 stage points (first
+        steps[r] steps) of ds w_stage max |d alpha| under relative input
+        perturbations eta -- how far tau moves when the warm alpha's inputs move
+        by a few tens of ulps (the C5 parity bar's a-priori conditioning flag)."""
+        x0, N0 = _c(x0).reshape(-1, 3), _c(N0).reshape(-1, 3)
+        n = x0.shape[0]
+        st = np.ascontiguousarray(steps, dtype=np.int32)
+        out = np.zeros(n)
+        lib().or_warm_sensitivity(self.ref, C.c_double(omega), C.c_int(mode), C.c_int(iwarm),
+                                  C.c_double(ds), n, _p(x0), _p(N0), st.ctypes.data_as(_ip),
+                                  C.c_double(eta), _p(out), n_threads or default_threads())
+        return out
+
     def alpha_approx(self, x, N, omega, mode):
         return lib().or_alpha_approx(self.ref, _p(_c(x)), _p(_c(N)), C.c_double(omega),
                                      C.c_int(mode))

@@ -1167,6 +1167,78 @@ static void rhs(const or_plasma *p, const double u[6], double omega, int mode, i
     *alpha = alpha_model(p, u, omega, mode, absorb);
 }
 
+/* A-priori sensitivity of a warm-model trace's optical depth (test
+ * infrastructure for the C5 parity bar).  For each ray, over its
+ * first steps[r] fixed RK4 steps (the trajectory is alpha-independent), every
+ * stage point's warm alpha is re-evaluated at inputs perturbed by a relative eta
+ * -- Y up and down (the harmonic resonance makes alpha steepest in Y), and
+ * (X, N_par, Te) jointly both ways -- and the largest change, with the RK4
+ * weight ds/6 (1, 2, 2, 1), is summed: out_sens[r] = sum |d tau|.  A ray whose
+ * tau moves by more than the parity bar under perturbations of a few tens of
+ * ulps has a tau that no double-precision restatement determines to that bar:
+ * the fsup recurrence's cancellation (:536-557) at cold plasma edges, or a
+ * stage point sitting on a discontinuity of warmdisp's root selection (the
+ * selector test rr.re <= 0 of :1203-1214 decided at the 1e-11 level), where
+ * one ulp of Y picks the other root.  The flag depends on the shared trajectory
+ * only, not on the result of the implementation under test. */
+static void warm_inputs(const or_plasma *p, const double u[6], double omega, int mode, double *X,
+                        double *Y, double *Nabs, double *Npar, double *Te, double *inv) {
+    double b[3];
+    or_eval_plasma(p, u, u + 3, omega, X, Y, Npar, b);
+    *Nabs = sqrt(u[3] * u[3] + u[4] * u[4] + u[5] * u[5]);
+    *inv = 1.0 / or_grad_norm(p, u, u + 3, omega, mode);
+    *Te = or_T_e(p, u);
+}
+
+static double warm_stage_sens(const or_plasma *p, const double u[6], double omega, int mode,
+                              int iwarm, double eta) {
+    double X, Y, Nabs, Npar, Te, inv;
+    warm_inputs(p, u, omega, mode, &X, &Y, &Nabs, &Npar, &Te, &inv);
+    const double a0 = or_alpha_warm(omega, X, Y, Nabs, Npar, Te, inv, mode, iwarm, NULL);
+    static const double f[4][4] = {{0, 1, 0, 0}, {0, -1, 0, 0}, {1, 0, 1, -1}, {-1, 0, -1, 1}};
+    double d = 0.0;
+    for (int k = 0; k < 4; k++) {
+        const double a = or_alpha_warm(omega, X * (1.0 + eta * f[k][0]), Y * (1.0 + eta * f[k][1]), Nabs,
+                                       Npar * (1.0 + eta * f[k][2]), Te * (1.0 + eta * f[k][3]), inv,
+                                       mode, iwarm, NULL);
+        const double e = fabs(a - a0);
+        if (!(e <= d)) d = e;  /* NaN propagates as "unbounded" */
+    }
+    return d;
+}
+
+void or_warm_sensitivity(const or_plasma *p, double omega, int mode, int iwarm, double ds,
+                         int n_rays, const double *x0, const double *N0, const int *steps,
+                         double eta, double *out_sens, int n_threads) {
+    int nth = n_threads > 0 ? n_threads : 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nth)
+#endif
+    for (int r = 0; r < n_rays; r++) {
+        double u[6], sens = 0.0;
+        for (int k = 0; k < 3; k++) {
+            u[k] = x0[3 * r + k];
+            u[3 + k] = N0[3 * r + k];
+        }
+        for (int s = 0; s < steps[r]; s++) {
+            double k1[6], k2[6], k3[6], k4[6], ut[6], dummy;
+            rhs(p, u, omega, mode, 0, k1, &dummy);
+            sens += ds / 6.0 * warm_stage_sens(p, u, omega, mode, iwarm, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + 0.5 * ds * k1[k];
+            rhs(p, ut, omega, mode, 0, k2, &dummy);
+            sens += ds / 3.0 * warm_stage_sens(p, ut, omega, mode, iwarm, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + 0.5 * ds * k2[k];
+            rhs(p, ut, omega, mode, 0, k3, &dummy);
+            sens += ds / 3.0 * warm_stage_sens(p, ut, omega, mode, iwarm, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + ds * k3[k];
+            rhs(p, ut, omega, mode, 0, k4, &dummy);
+            sens += ds / 6.0 * warm_stage_sens(p, ut, omega, mode, iwarm, eta);
+            for (int k = 0; k < 6; k++) u[k] = u[k] + ds / 6.0 * (k1[k] + 2.0 * k2[k] + 2.0 * k3[k] + k4[k]);
+        }
+        out_sens[r] = sens;
+    }
+}
+
 /* shell index j with grid[j] <= v < grid[j+1]; clamps to [0, n-2] */
 static int shell_of(const double *g, int n, double v) {
     int lo = 0, hi = n - 1;

@@ -171,6 +171,12 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
  * (src/solve.jl:164-172): out_samples n_rays x (n_steps+1) x 3 =
  * (psi(x_k), dP/ds_k = P_k alpha_approx(x_k, N_k), s_k) for k = 0 (entry
  * point, dP/ds = 0 as the reference's initial vector, :151) .. steps; NaN beyond. */
+/* a-priori sensitivity of warm traces' optical depths to relative input
+ * perturbations eta at every RK4 stage point (see torj_oracle.c): out_sens[r] =
+ * sum over ray r's stages (first steps[r] steps) of ds w_stage max |d alpha| */
+void or_warm_sensitivity(const or_plasma *p, double omega, int mode, int iwarm, double ds,
+                         int n_rays, const double *x0, const double *N0, const int *steps,
+                         double eta, double *out_sens, int n_threads);
 int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
                      const double *N0, const double *weights, double *out_state, int *out_status,
                      int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,
