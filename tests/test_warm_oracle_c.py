@@ -134,3 +134,67 @@ def test_warm_trace_threads_bitwise(O, oplasma):
     b = oplasma.trace(xs, Ns, om, 1, 1e-3, 200, n_threads=4, **kw)
     for k in ("state", "status", "steps", "Pdep"):
         assert np.array_equal(a[k], b[k]), k
+
+
+def _c5_rays(idx):
+    """entry states of fan rays of the C5 beam (92 / 11 fan, X-mode 92.5 GHz)"""
+    import torj_hip as T
+    from torj_hip import synthetic as S
+
+    eq = S.circular_tokamak()
+    P = T.Plasma(*S.plasma_args(eq))
+    s = S.SETUP
+    f = s["f_abs_test"]
+    N0 = T.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=92,
+                                            min_azimuthal_points=11)
+    om = 2 * np.pi * f
+    xp, Np, s0, st = T.ray_entry(P, pos[idx], dirs[idx], om, 1)
+    assert (st == 0).all()
+    return xp, Np, om
+
+
+def test_c5_conditioning_flag_and_the_50_digit_evidence(O, oplasma):
+    """The C5 parity bar's a-priori flag (oracle or_warm_sensitivity, bench.py):
+    fan rays 94302 and 89686 -- out of the 1e-8 bar GPU vs oracle in round 2 --
+    are flagged, a well-conditioned ray (20731) is not.  And the reason, pinned
+    at ray 94302's stage point 136 (Te 31 eV, Y = 0.50019, a cold-edge second-
+    harmonic crossing): the reference's algorithm is discontinuous there -- one
+    ulp less Y takes warmdisp's root selector to the other root (warm_ref: alpha
+    0.774 -> 9.7e-5 /m) -- while the 50-digit evaluation (oracle/warm_mp.py)
+    gives the branch the neighbouring stage points continue (0.7739 /m)."""
+    import warm_mp
+    import warm_ref
+
+    idx = np.array([94302, 89686, 20731])
+    xp, Np, om = _c5_rays(idx)
+    r = oplasma.trace(xp, Np, om, 1, 1e-4, 2000, absorption=2)
+    sens = oplasma.warm_sensitivity(xp, Np, om, 1, 1e-4, r["steps"])
+    rel = sens / np.maximum(np.abs(r["state"][:, 6]), 1e-6)
+    assert rel[0] > 0.5e-8 and rel[1] > 0.5e-8 and rel[2] < 0.5e-8, rel
+    # stage point 136 of ray 94302, recorded through the oracle's alpha hook
+    pts = []
+
+    def fn(omega, X, Y, Nabs, Npar, Te, inv, mode, model):
+        pts.append((omega, X, Y, Nabs, Npar, Te, inv))
+        return O.alpha_warm(omega, X, Y, Nabs, Npar, Te, inv, mode, 1)[0]
+
+    hook = O._ALPHA_FN(fn)
+    install = O._install_warm_hook
+    O._install_warm_hook = lambda on: O.lib().or_set_alpha_hook(hook)
+    try:
+        oplasma.trace(xp[:1], Np[:1], om, 1, 1e-4, 40, absorption=2, n_threads=1)
+    finally:
+        O._install_warm_hook = install
+        O.lib().or_set_alpha_hook(None)
+    p = list(pts[136])
+    assert 30 < p[5] < 33 and abs(p[2] - 0.5002) < 1e-4
+    a, _ = warm_ref.alpha_warm(*p, 1, 1)
+    q = list(p)
+    q[2] = np.nextafter(p[2], 0.0)
+    a_down, _ = warm_ref.alpha_warm(*q, 1, 1)
+    assert a > 0.7 and a_down < 1e-3  # one ulp of Y: the other root
+    mp = float(warm_mp.alpha_warm_wr(*p, 1))
+    prev = float(warm_mp.alpha_warm_wr(*pts[135], 1))
+    assert abs(mp - 0.7739104) < 1e-6 and abs(prev - mp) < 1e-4 * mp
