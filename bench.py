@@ -317,6 +317,13 @@ def main():
                 "flop_per_launch": flop,
                 "flop_source": flop_source if flop is not None else None,
                 "flop_per_ray_step": flop / max(cnt[0], 1) if flop is not None else None,
+                # the same launch priced as the reference's algorithm, which evaluates the
+                # integrals the kernel skips bit-identically (exact zeros, negligible ones)
+                "flop_per_launch_reference_algorithm": (
+                    F.algorithmic_flops_reference(cnt, n_gl=24) if args.absorption == "albajar" else None),
+                "frac_reference_algorithm": (
+                    F.algorithmic_flops_reference(cnt, n_gl=24) / kern_s / 1e12 / FP64_VECTOR_PEAK_TFLOPS
+                    if args.absorption == "albajar" else None),
             },
             "work_counters": (
                 {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),

@@ -44,6 +44,24 @@ def algorithmic_flops(counters, n_gl: int = 24) -> float:
             + FLOPS_SERIES_TERM * (terms - harm * pairs))
 
 
+def algorithmic_flops_reference(counters, n_gl: int = 24) -> float:
+    """The same launch priced as the reference's algorithm (the CPU restatement,
+    SURVEY.md §8(d)): every harmonic integral with m >= m_0 evaluated with its
+    full node loop -- the exactly-zero and the negligible integrals the kernel
+    skips (bit-identically) at the cost of an evaluated one, with the shortest
+    Bessel polynomial (7 terms; a lower bound).  A figure beside
+    algorithmic_flops, never instead of it: the roofline fraction is priced on
+    the work the kernel does."""
+    zero = float(counters[5]) if len(counters) > 5 else 0.0
+    negl = float(counters[6]) if len(counters) > 6 else 0.0
+    pairs = (n_gl + 1) // 2
+    skipped = zero + negl
+    return (algorithmic_flops(counters, n_gl)
+            - zero * (FLOPS_HARM + FLOPS_ZERO_TEST) - negl * (FLOPS_HARM + FLOPS_ZERO_TEST + FLOPS_NEGL_TEST)
+            + skipped * (FLOPS_HARM + pairs * FLOPS_PAIR_SHARED + n_gl * FLOPS_NODE
+                         + FLOPS_SERIES_TERM * pairs * (7 - 1)))
+
+
 # Weakly relativistic warm alpha (absorption 2, torj_warm.hpp alpha_warm_v<1>),
 # per trip, from the instrumented restatement `python oracle/flopcount_warm.py`
 # (same convention; factorial tables and loop invariants not counted; branch-
