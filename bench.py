@@ -44,8 +44,8 @@ ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n-rings", type=int, default=92)
     ap.add_argument("--min-az", type=int, default=11)
     ap.add_argument("--n-steps", type=int, default=2000)
@@ -318,7 +318,8 @@ def main():
                 "flop_source": flop_source if flop is not None else None,
                 "flop_per_ray_step": flop / max(cnt[0], 1) if flop is not None else None,
                 # the same launch priced as the reference's algorithm, which evaluates the
-                # integrals the kernel skips bit-identically (exact zeros, negligible ones)
+                # integrals the kernel skips bit-identically (exact zeros, negligible ones,
+                # the harmonics of calls settled before the polarisation vector)
                 "flop_per_launch_reference_algorithm": (
                     F.algorithmic_flops_reference(cnt, n_gl=24) if args.absorption == "albajar" else None),
                 "frac_reference_algorithm": (
@@ -335,7 +336,8 @@ def main():
                  "alpha_active": int(cnt[2]), "harmonic_integrals": int(cnt[3]),
                  "bessel_series_terms": int(cnt[4]),
                  "harmonic_integrals_exact_zero": int(cnt[5]),
-                 "harmonic_integrals_negligible": int(cnt[6])}),
+                 "harmonic_integrals_negligible": int(cnt[6]),
+                 "harmonic_integrals_settled_early": int(cnt[7])}),
         }
         if world == 1 and not args.no_host_api:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,

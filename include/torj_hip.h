@@ -213,7 +213,10 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
  *   absorption 1 (Albajar): [2] calls reaching the harmonic sum, [3] harmonic
  *     integrals evaluated, [4] Bessel-series terms, [5] harmonic integrals found
  *     exactly zero without their node loop, [6] harmonic integrals skipped as
- *     provably below an ulp of the sum (alpha bit-identical), [7] 0;
+ *     provably below an ulp of the sum (alpha bit-identical), [7] harmonic
+ *     integrals found exactly zero in calls settled before the polarisation
+ *     vector (every harmonic present an exact zero: alpha = 0, no call
+ *     reaches the harmonic sum);
  *   absorption 2 (warm, iwarm 1): [2] larmornumber tests, [3] Faddeeva
  *     evaluations, [4] warmdisp passes, [5] passes x Larmor order lrm,
  *     [6] sum lrm, [7] sum lrm^2 (one warm alpha per RHS evaluation);

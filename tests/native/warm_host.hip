@@ -77,6 +77,7 @@ void wh_albajar_work(int n, const double *om, const double *X, const double *Y, 
         torj::AlbajarWork w{};
         (void)torj::abs_albajar_fast(g_wh_gl, om[i], X[i], Y[i], Nabs[i], Npar[i], Te[i], mode, &w);
         work3[3 * i] = w.n_harm, work3[3 * i + 1] = w.n_zero, work3[3 * i + 2] = w.n_negl;
+        work3[3 * i + 1] |= w.n_early << 8;  // settled before the polarisation vector
     }
 }
 

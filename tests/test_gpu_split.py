@@ -284,5 +284,9 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
         assert np.array_equal(a.traj, b.traj, equal_nan=True)
         c0, c1 = cnts["0", sched], cnts["1", sched]
         assert c0[6] == 0 and c1[6] > 0.1 * c0[3], (c0, c1)
-        assert c1[3] + c1[6] == c0[3] and np.array_equal(c0[[0, 1, 2, 5]], c1[[0, 1, 2, 5]])
+        assert c1[3] + c1[6] == c0[3] and np.array_equal(c0[[0, 1]], c1[[0, 1]])
+        # calls settled before the polarisation vector (every harmonic present an
+        # exact zero): their harmonics leave the zero count for counter [7]
+        assert c0[7] == 0 and c1[7] > 0 and c1[2] < c0[2] and c1[5] < c0[5], (c0, c1)
+        assert c1[5] + c1[7] >= c0[5], (c0, c1)
     assert np.array_equal(cnts["1", 3], cnts["1", 0])

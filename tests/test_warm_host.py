@@ -172,7 +172,11 @@ def test_albajar_negligible_harmonic_skip_is_bit_identical(H):
     the harmonics already summed (torj_math.hpp albajar_harmonic) leaves
     abs_Albajar_fast bit-identical: host build with the skip on and off over
     stage points along rays of the headline fan (where the third harmonic is
-    summed beside the second) and the oracle's golden sweep; the skip fires."""
+    summed beside the second) and the oracle's golden sweep; the skip fires.
+    The same switch settles a call before its polarisation vector when every
+    harmonic present is an exact zero: alpha is then a zero of either sign (the
+    full evaluation's -0 or the early +0; no later operation sees the sign), so
+    zeros are compared as zeros and every other value bit for bit."""
     import json
 
     rows = _stage_points()
@@ -182,7 +186,7 @@ def test_albajar_negligible_harmonic_skip_is_bit_identical(H):
     H.wh_albajar_work.argtypes = [C.c_int] + [_dp] * 6 + [C.c_int, C.POINTER(C.c_uint)]
     H.wh_set_negl_skip.argtypes = [C.c_int]
     t, w = np.polynomial.legendre.leggauss(24)
-    skipped = 0
+    skipped = early = 0
     for pts, mode in ((rows, 1), (g[g[:, 6] == 1][:, :6], 1), (g[g[:, 6] == -1][:, :6], -1)):
         n = len(pts)
         cols = [np.ascontiguousarray(pts[:, k]) for k in range(6)]
@@ -195,10 +199,18 @@ def test_albajar_negligible_harmonic_skip_is_bit_identical(H):
             wk = np.zeros(3 * n, dtype=np.uint32)
             H.wh_albajar_work(n, *[_d(c) for c in cols], mode, wk.ctypes.data_as(C.POINTER(C.c_uint)))
             out[on] = (a, wk.reshape(-1, 3))
-        assert np.array_equal(out[1][0].view(np.int64), out[0][0].view(np.int64))
-        assert out[0][1][:, 2].sum() == 0
-        # every skipped integral is one the no-skip run evaluated
+        assert np.array_equal((out[1][0] + 0.0).view(np.int64), (out[0][0] + 0.0).view(np.int64))
+        assert out[0][1][:, 2].sum() == 0 and (out[0][1][:, 1] >> 8).sum() == 0
+        # every skipped integral is one the no-skip run evaluated; a call settled
+        # early is one whose harmonics the no-skip run found exactly zero or never
+        # reached (the polarisation's own early returns: N_par^2 >= 1, X >= 1 ...)
         assert out[1][1][:, 0].sum() + out[1][1][:, 2].sum() == out[0][1][:, 0].sum()
+        on_zero, on_early = out[1][1][:, 1] & 0xFF, out[1][1][:, 1] >> 8
+        assert np.all(on_zero + np.minimum(on_early, out[0][1][:, 1]) == out[0][1][:, 1])
+        assert np.all(out[0][1][on_early > 0, 0] == 0)
+        assert np.all(out[1][0][on_early > 0] == 0.0)
         skipped += int(out[1][1][:, 2].sum())
+        early += int((on_early > 0).sum())
     H.wh_set_negl_skip(1)
     assert skipped > 0.2 * len(rows)
+    assert early > 0.1 * len(rows)

@@ -397,7 +397,7 @@ __device__ __forceinline__ void flush_counters(const TraceArgs &a, unsigned long
     // [6]: Albajar's negligible-harmonic skips, or the warm model's sum of lrm
     // (each model leaves the other's field 0)
     const unsigned long long s6 = wave_sum((unsigned long long)(work.n_l + work.n_negl));
-    const unsigned long long s7 = wave_sum((unsigned long long)work.n_l2);
+    const unsigned long long s7 = wave_sum((unsigned long long)(work.n_l2 + work.n_early));
     if ((threadIdx.x & 63) == 0) {
         atomicAdd(a.counters + 0, s0);
         atomicAdd(a.counters + 1, s1);
@@ -1110,7 +1110,7 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     if (sp.awork)  // a counted launch (null otherwise: no work words written or read)
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
-                                     ((work.n_negl & 3u) << 16);
+                                     ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
 }
 
 // the warm alpha (absorption 2 / 3, iwarm 1 / 3) at the stored stage points:
@@ -1209,6 +1209,7 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
                         c5 += (wk >> 3) & 3u;
                         c4 += (wk >> 5) & 2047u;
                         c6 += (wk >> 16) & 3u;
+                        c7 += (wk >> 18) & 3u;
                     } else if (am == 2) {
                         const unsigned lrm = wk >> 21, passes = (wk >> 14) & 127u;
                         c2 += wk & 127u;

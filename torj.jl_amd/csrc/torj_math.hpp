@@ -730,6 +730,43 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     return s;
 }
 
+// The geometry of harmonic m's resonance ellipse that needs no polarisation:
+// gamma(t)^2 = C0 + C1 t^2 +- C2 t over the node pairs, gamma_min^2 = qmin, and
+// whether the whole node sum underflows to an exact zero (albajar_harmonic).
+// Depends on (mu, r = m / m_0, N_par) only, so abs_albajar_fast_body computes it
+// before the polarisation vector and can settle alpha = 0 there.
+struct HarmGeom {
+    double r, r2m1, sq_r, upa0, upa1, C0, C1, C2, qmin;
+    bool zero;
+};
+
+TORJ_HD HarmGeom harm_geom(double mu, double r, double Npar, double inv_sqNp) {
+    HarmGeom g;
+    g.r = r;
+    g.r2m1 = r * r - 1.0;
+    g.sq_r = sqrt_nn(g.r2m1);
+    g.upa0 = inv_sqNp * r * Npar;
+    g.upa1 = inv_sqNp * g.sq_r;
+    g.C0 = fma(g.upa0, g.upa0, r * r);
+    g.C1 = g.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
+    g.C2 = 2.0 * g.upa0 * g.upa1;
+    // Exact zero: every node's exp(mu (1 - gamma)) underflows to +0 (exp_fast
+    // returns exactly 0 below -746) when mu (gamma_min - 1) exceeds 760, gamma_min
+    // the least gamma(t) = sqrt(C0 + C1 t^2 + C2 t) over t in [-1, 1] (a bound
+    // for every node of both signs, the vertex of the parabola or an end); the
+    // margin of 14 covers the rounding of gamma^2 and mu (1 - gamma).  Then every
+    // pair term is w p (P (0 + 0) + t Q (0 - 0)) = +-0 and the node sum is +-0:
+    // the loop is skipped with the same value (the sign of a zero aside, which
+    // no later operation sees) -- far from the resonance that is most of the
+    // third harmonic's evaluations on a beam.  NaN operands never skip.
+    const double qe = fma(g.C1, 1.0, g.C0) - fabs(g.C2);  // min of the ends t = -1, 1
+    const double tv = -g.C2 * 0.5 * rcp_nz(g.C1);          // vertex (C1 > 0)
+    const double qv = fma(-0.25 * g.C2, g.C2 * rcp_nz(g.C1), g.C0);
+    g.qmin = (g.C1 > 0.0 && fabs(tv) <= 1.0) ? qv : qe;
+    g.zero = g.qmin > 1.0 && mu * (sqrt_nn(g.qmin) - 1.0) > 760.0;
+    return g;
+}
+
 // Work counters of one lane (include/torj_hip.h torj_trace: counters[2..7]).
 // Albajar (ABS 1) / warm weakly relativistic (ABS 2, torj_warm.hpp) meaning:
 struct AlbajarWork {
@@ -740,20 +777,21 @@ struct AlbajarWork {
     uint32_t n_l;       // - / sum of Larmor orders lrm
     uint32_t n_l2;      // - / sum of lrm^2
     uint32_t n_negl;    // harmonic integrals skipped as below an ulp of the sum / -
+    uint32_t n_early;   // exact-zero harmonics of calls settled before the polarisation vector / -
 };
 
 // Resonance-ellipse integral for harmonic m (abs_Al_integral_nume_fast +
 // abs_Al_pol_fact) times sqrt((m/m_0)^2 - 1), WITHOUT the Maxwellian
 // normalisation a*(mu/2pi)^1.5 (common to both harmonics).
 template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
-TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double Npar,
+TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg,
                                 double inv_sqNp, double N_perp, double omega_bar,
                                 double Axz, double ea, double e3, AlbajarWork *work, int sub = 0,
                                 double dom = 0.0) {
     constexpr double md = (double)M, inv_md = 1.0 / md;
     HarmConst c;
-    c.r2m1 = r * r - 1.0;
-    const double sq_r = sqrt_nn(c.r2m1);
+    c.r2m1 = hg.r2m1;
+    const double sq_r = hg.sq_r;
     c.x_m = N_perp * omega_bar * sq_r;
     const double q = c.x_m * inv_sqNp * inv_md;  // x_m / (m sqrt(1 - N_par^2))
     c.K0 = Axz * Axz + ea * ea;
@@ -762,27 +800,15 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, double r, double N
     c.K3 = q * q * e3 * e3;
     c.K4 = 2.0 * q * Axz * e3;
     c.K5 = q * ea * e3 * c.x_m * inv_md;
-    c.upa0 = inv_sqNp * r * Npar;
-    c.upa1 = inv_sqNp * sq_r;
+    c.upa0 = hg.upa0;
+    c.upa1 = hg.upa1;
     c.mu = mu;
-    c.C0 = fma(c.upa0, c.upa0, r * r);
-    c.C1 = c.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
-    c.C2 = 2.0 * c.upa0 * c.upa1;
+    c.C0 = hg.C0;
+    c.C1 = hg.C1;
+    c.C2 = hg.C2;
     c.hx = 0.5 * c.x_m;
-    // Exact zero: every node's exp(mu (1 - gamma)) underflows to +0 (exp_fast
-    // returns exactly 0 below -746) when mu (gamma_min - 1) exceeds 760, gamma_min
-    // the least gamma(t) = sqrt(C0 + C1 t^2 + C2 t) over t in [-1, 1] (a bound
-    // for every node of both signs, the vertex of the parabola or an end); the
-    // margin of 14 covers the rounding of gamma^2 and mu (1 - gamma).  Then every
-    // pair term is w p (P (0 + 0) + t Q (0 - 0)) = +-0 and the node sum is +-0:
-    // the loop is skipped with the same value (the sign of a zero aside, which
-    // no later operation sees) -- far from the resonance that is most of the
-    // third harmonic's evaluations on a beam.  NaN operands never skip.
-    const double qe = fma(c.C1, 1.0, c.C0) - fabs(c.C2);  // min of the ends t = -1, 1
-    const double tv = -c.C2 * 0.5 * rcp_nz(c.C1);          // vertex (C1 > 0)
-    const double qv = fma(-0.25 * c.C2, c.C2 * rcp_nz(c.C1), c.C0);
-    const double qmin = (c.C1 > 0.0 && fabs(tv) <= 1.0) ? qv : qe;
-    const bool zero = qmin > 1.0 && c.mu * (sqrt_nn(qmin) - 1.0) > 760.0;
+    const double qmin = hg.qmin;
+    const bool zero = hg.zero;  // the exact-zero bound (harm_geom)
     // Bessel polynomial from the largest argument x_m (SeriesCoefs: x_m <= 1,
     // 2, 3, 4, each within a few ulp of mpmath's J_nu, checked in tests; the
     // 44-term Taylor loop beyond); physical rays have x_m < m.  The level is made
@@ -870,19 +896,37 @@ struct AlbPro {
     double inv_mu, mu, omega_bar, N_perp, inv_sqNp, Axz, ea, e3, m_0, inv_m0;
 };
 
-TORJ_HD AlbPro albajar_prologue(double X, double Y, double N_abs, double N_par, double Te,
+// The polarisation-free part of the prologue (Te >= 20): what the harmonics'
+// resonance geometry (harm_geom) needs, computed before the polarisation vector.
+struct AlbPre {
+    double inv_mu, mu, omega_bar, N_perp, sqNp, m_0, inv_sqNp, inv_m0;
+};
+TORJ_HD AlbPre albajar_pre(double Y, double N_abs, double N_par, double Te) {
+    AlbPre p;
+    constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te
+    p.inv_mu = Te * (1.0 / kMuTe);
+    p.mu = kMuTe * rcp_nz(Te);
+    p.omega_bar = rcp_nz(Y);
+    p.N_perp = sqrt_nn(N_abs * N_abs - N_par * N_par);
+    const double omNp2 = 1.0 - N_par * N_par;
+    p.sqNp = sqrt_nn(omNp2);
+    p.m_0 = p.sqNp * p.omega_bar;
+    p.inv_sqNp = rcp_nz(p.sqNp);
+    p.inv_m0 = p.inv_sqNp * Y;
+    return p;
+}
+
+TORJ_HD AlbPro albajar_prologue(const AlbPre &pre, double X, double Y, double N_abs, double N_par,
                                 int mode) {
     AlbPro q;
     q.ok = false;
-    if (Te < 20.0) return q;
-    constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te
-    q.inv_mu = Te * (1.0 / kMuTe);
-    q.mu = kMuTe * rcp_nz(Te);
-    const double omega_bar = rcp_nz(Y);
+    q.inv_mu = pre.inv_mu;
+    q.mu = pre.mu;
+    const double omega_bar = pre.omega_bar;
     q.omega_bar = omega_bar;
     const double cos_t = N_par * rcp_nz(N_abs);
     const double sin_t = sqrt_nn(fma(-cos_t, cos_t, 1.0));
-    const double N_perp = sqrt_nn(N_abs * N_abs - N_par * N_par);
+    const double N_perp = pre.N_perp;
     q.N_perp = N_perp;
     // abs_Al_N_with_pol_vec (src/absorption.jl:10-64), real form:
     // e = (e1, i*ea, e3) with e1, ea, e3 real.
@@ -920,15 +964,13 @@ TORJ_HD AlbPro albajar_prologue(double X, double Y, double N_abs, double N_par, 
         e1 = -(omega_bar * g) * ea;
         e3 = -((Nt2 * sin_t * cos_t) * inv_den) * e1;
     }
-    const double omNp2 = 1.0 - N_par * N_par;
-    const double sqNp = sqrt_nn(omNp2);
-    q.m_0 = sqNp * omega_bar;
-    q.inv_sqNp = rcp_nz(sqNp);
+    q.m_0 = pre.m_0;
+    q.inv_sqNp = pre.inv_sqNp;
     const double N_eff = (N_perp * N_par) * (q.inv_sqNp * q.inv_sqNp);
     q.Axz = e1 + N_eff * e3;
     q.ea = ea;
     q.e3 = e3;
-    q.inv_m0 = q.inv_sqNp * Y;
+    q.inv_m0 = pre.inv_m0;
     q.ok = true;
     return q;
 }
@@ -936,12 +978,11 @@ TORJ_HD AlbPro albajar_prologue(double X, double Y, double N_abs, double N_par, 
 // harmonic m of the sum (src/absorption.jl:213-223), if m >= m_0 (NaN m_0: no
 // harmonic, as the reference's `m < m_0` test makes it)
 template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
-TORJ_HD double albajar_pro_harmonic(const GLTable &gl, const AlbPro &q, double N_par,
+TORJ_HD double albajar_pro_harmonic(const GLTable &gl, const AlbPro &q, const HarmGeom &hg,
                                     AlbajarWork *work, int sub = 0, double dom = 0.0) {
     const uint32_t z0 = work ? work->n_zero + work->n_negl : 0u;
-    const double h = albajar_harmonic<M, LPR, U>(gl, q.mu, (double)M * q.inv_m0, N_par, q.inv_sqNp,
-                                                 q.N_perp, q.omega_bar, q.Axz, q.ea, q.e3, work, sub,
-                                                 dom);
+    const double h = albajar_harmonic<M, LPR, U>(gl, q.mu, hg, q.inv_sqNp, q.N_perp, q.omega_bar,
+                                                 q.Axz, q.ea, q.e3, work, sub, dom);
     if (work && work->n_zero + work->n_negl == z0) work->n_harm++;
     return h;
 }
@@ -960,12 +1001,32 @@ template <int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, double Y,
                                      double N_abs, double N_par, double Te, int mode,
                                      AlbajarWork *work, int sub = 0) {
-    const AlbPro q = albajar_prologue(X, Y, N_abs, N_par, Te, mode);
+    if (Te < 20.0) return 0.0;
+    const AlbPre pre = albajar_pre(Y, N_abs, N_par, Te);
+    const bool h2 = !(2.0 < pre.m_0), h3 = !(3.0 < pre.m_0);  // harmonic m present iff m >= m_0
+    HarmGeom g2{}, g3{};
+    if (h2) g2 = harm_geom(pre.mu, 2.0 * pre.inv_m0, N_par, pre.inv_sqNp);
+    if (h3) g3 = harm_geom(pre.mu, 3.0 * pre.inv_m0, N_par, pre.inv_sqNp);
+    // Settled before the polarisation vector: when every harmonic present is an
+    // exact zero (harm_geom), alpha is a zero whatever the polarisation -- the
+    // harmonics would return -mu Pm^2 0 sq_r, finite and zero because N_perp and
+    // omega_bar are finite and positive and sq_r is finite, and the prologue's own
+    // early returns are zeros too -- so the polarisation vector, the harmonics'
+    // K coefficients and the normalisation are skipped (44 % of the stage points
+    // of the headline beam: edge plasma and far from every resonance).  Off with
+    // the negligible-harmonic skip (GLTable::negl_skip, TORJ_NEGL_SKIP=0).
+    if (gl.negl_skip && pre.N_perp > 0.0 && pre.N_perp < INFINITY && pre.omega_bar > 0.0 &&
+        pre.omega_bar < INFINITY && pre.mu < INFINITY &&
+        (!h2 || (g2.zero && g2.sq_r < INFINITY)) && (!h3 || (g3.zero && g3.sq_r < INFINITY))) {
+        if (work) work->n_early += (uint32_t)h2 + (uint32_t)h3;
+        return 0.0;
+    }
+    const AlbPro q = albajar_prologue(pre, X, Y, N_abs, N_par, mode);
     if (!q.ok) return 0.0;
     if (work) work->n_active++;
     double c_abs = 0.0;
-    if (!(2.0 < q.m_0)) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, N_par, work, sub);
-    if (!(3.0 < q.m_0)) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, N_par, work, sub, c_abs);
+    if (h2) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, g2, work, sub);
+    if (h3) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, g3, work, sub, c_abs);
     return albajar_finish(q, c_abs, X, omega);
 }
 // the fused trace kernels' call (out of line there, see TORJ_ALB_ATTR); kernels

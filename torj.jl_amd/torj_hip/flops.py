@@ -27,16 +27,22 @@ FLOPS_NEGL_TEST = 59        # per harmonic skipped as below an ulp of the sum (t
                             # exp(mu (1 - gamma_min)) (26 + 3) -- on top of FLOPS_HARM and the
                             # gamma_min test; the node loop it skips is not counted.  Tests that
                             # do not skip cost the same and are not counted (conservative).
+FLOPS_EARLY_HARM = 27       # per harmonic of a call settled before the polarisation vector
+                            # (torj_math.hpp harm_geom: r, sqrt(r^2 - 1), u_par0/1, C0..C2 (15)
+                            # and the gamma_min test (12)); the call's own prologue
+                            # (mu, omega_bar, N_perp, m_0: 12) is not counted (conservative).
 
 
 def algorithmic_flops(counters, n_gl: int = 24) -> float:
     """counters = (ray_steps, rhs_evals, alpha_active, harmonic_integrals, series_terms
-    [, harmonic_integrals_exact_zero [, harmonic_integrals_negligible]])."""
+    [, harmonic_integrals_exact_zero [, harmonic_integrals_negligible
+    [, harmonic_integrals_settled_early]]])."""
     steps, rhs, act, harm, terms = (float(c) for c in counters[:5])
     zero = float(counters[5]) if len(counters) > 5 else 0.0
     negl = float(counters[6]) if len(counters) > 6 else 0.0
+    early = float(counters[7]) if len(counters) > 7 else 0.0
     pairs = (n_gl + 1) // 2
-    return (steps * FLOPS_STEP_OVERHEAD + rhs * FLOPS_RHS_COLD
+    return (steps * FLOPS_STEP_OVERHEAD + rhs * FLOPS_RHS_COLD + early * FLOPS_EARLY_HARM
             + act * (FLOPS_ALPHA_PRE + FLOPS_ALPHA_POST)
             + harm * (FLOPS_HARM + pairs * FLOPS_PAIR_SHARED + n_gl * FLOPS_NODE)
             + zero * (FLOPS_HARM + FLOPS_ZERO_TEST)
@@ -49,15 +55,18 @@ def algorithmic_flops_reference(counters, n_gl: int = 24) -> float:
     SURVEY.md §8(d)): every harmonic integral with m >= m_0 evaluated with its
     full node loop -- the exactly-zero and the negligible integrals the kernel
     skips (bit-identically) at the cost of an evaluated one, with the shortest
-    Bessel polynomial (7 terms; a lower bound).  A figure beside
+    Bessel polynomial (7 terms; a lower bound), and the calls settled before
+    the polarisation vector priced by their harmonics alone.  A figure beside
     algorithmic_flops, never instead of it: the roofline fraction is priced on
     the work the kernel does."""
     zero = float(counters[5]) if len(counters) > 5 else 0.0
     negl = float(counters[6]) if len(counters) > 6 else 0.0
+    early = float(counters[7]) if len(counters) > 7 else 0.0
     pairs = (n_gl + 1) // 2
-    skipped = zero + negl
+    skipped = zero + negl + early
     return (algorithmic_flops(counters, n_gl)
             - zero * (FLOPS_HARM + FLOPS_ZERO_TEST) - negl * (FLOPS_HARM + FLOPS_ZERO_TEST + FLOPS_NEGL_TEST)
+            - early * FLOPS_EARLY_HARM
             + skipped * (FLOPS_HARM + pairs * FLOPS_PAIR_SHARED + n_gl * FLOPS_NODE
                          + FLOPS_SERIES_TERM * pairs * (7 - 1)))
 
