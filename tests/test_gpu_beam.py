@@ -241,9 +241,10 @@ def test_c4_million_ray_beam_sharded_rccl_batched(gpu, T, hplasma, oplasma):
     the per-launch workspace capped at 4 GiB (TORJ_WS_GB) so every shard runs in
     ray batches.  Every 250th ray vs the CPU oracle at the parity bar (status
     and steps exact, x, N, tau 1e-10); per-ray outputs bit-identical to one
-    unsplit torj_trace_ex launch of the beam (its own 16 GiB batches; both on the
-    split pipeline, forced by set_sched(3), so every wave holds the same rays),
-    dP_shell to its summation order."""
+    unsplit torj_trace_ex launch of the beam (one launch under the default
+    workspace budget, half the free device memory; both on the split pipeline,
+    forced by set_sched(3), so every wave holds the same rays), dP_shell to its
+    summation order."""
     from test_gpu_parity import _compare_trace
     from torj_hip import synthetic as S
 

@@ -2561,11 +2561,20 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
 // shell arrays: ~116 KB per ray at 2 000 steps and 1 000 shells).  A beam whose
 // workspace would exceed it is traced in contiguous batches of whole 64-ray
 // groups, each batch's inputs gathered into and outputs scattered from
-// compact device buffers (TORJ_WS_GB, default 16).
-static size_t ws_budget() {
-    const char *e = getenv("TORJ_WS_GB");  // read per call (tests vary it)
-    const double g = e ? atof(e) : 16.0;
-    return (size_t)(g * (double)(1ull << 30));
+// compact device buffers.  TORJ_WS_GB (read per call, tests vary it) sets the
+// budget; by default it is half of the device memory this handle could use
+// (free + its own fit workspace, which a larger one replaces), at least 16 GiB:
+// on a 288 GB MI355X the 1e6-ray C4 beam (~116 GB) then runs as one launch
+// (606 against 675 ms in seven 16 GiB batches, each with its own pipeline fill
+// and drain), with room left for the split ring and the caller's buffers.
+// The device must be current (ensure_device).
+static size_t ws_budget(const torj_plasma_s *p) {
+    const char *e = getenv("TORJ_WS_GB");
+    if (e) return (size_t)(atof(e) * (double)(1ull << 30));
+    const size_t floor16 = 16ull << 30;
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return floor16;
+    return std::max(floor16, (free_b + p->fit_cap) / 2);
 }
 
 static int ensure_batch(torj_plasma_s *p, size_t bytes) {
@@ -2593,9 +2602,10 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     if (fit && cfg->n_steps > 0 && x0 && N0 && state && status && steps) {
         const size_t K = (size_t)cfg->n_steps + 2, L = (size_t)n_psi;
         const size_t per_ray = (cfg->integrator == 1 ? 6 : 5) * 8 * K + 4 * (L + 1) + 16 * L + 4;
-        if ((size_t)n * per_ray > ws_budget()) {
-            const int nb = (int)std::max<size_t>(64, ws_budget() / per_ray / 64 * 64);
-            if (ensure_device(p)) return -1;
+        if (ensure_device(p)) return -1;
+        const size_t budget = ws_budget(p);
+        if ((size_t)n * per_ray > budget) {
+            const int nb = (int)std::max<size_t>(64, budget / per_ray / 64 * 64);
             hipStream_t s = (hipStream_t)stream;
             const int n_save = cfg->traj_stride > 0 && traj ? cfg->n_steps / cfg->traj_stride : 0;
             const size_t D = sizeof(double), B = (size_t)nb;
