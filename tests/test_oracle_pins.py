@@ -389,3 +389,39 @@ def test_deposition_ref_pinned_on_analytic_profile():
     prof2, _ = D.power_deposition_profile(s[m], psi(s[m]), dpds(s[m]), grid, lambda p: p)
     ex2 = exact(0.8)
     assert np.abs(prof2 - ex2).max() <= 1e-8 * np.abs(ex).max()
+
+
+def test_power_callback_never_fires_on_the_fans(O, oplasma, T, eq):
+    """make_ray's ContinuousCallback(u[7] < 0) (src/solve.jl:159-161, affect!
+    :78-83) acts only when an accepted step takes P below 0.  For dP/ds = -alpha P
+    with alpha frozen over a step, P_{n+1} = R(-h alpha) P_n, and neither
+    method's stability polynomial R has a real negative root (RK4's is the
+    quartic Taylor polynomial of e^z; Tsit5's, from the oracle's tableau, stays
+    >= 0.15 on the whole negative axis, its minimum at z = -2.15), so only
+    alpha's variation within one step could take P below 0.  The X-mode fan
+    (BASELINE C3, every 500th ray) peaks at alpha ~ 500 /m: with dtmax = 1e-4
+    (src/solve.jl:157) h alpha <= 0.05 and R(-h alpha) is within 1e-7 of
+    e^(-h alpha).  The callback does not fire on these beams, and where in a
+    step the reference would locate P = 0 (not reproduced) never
+    matters."""
+    from torj_hip import synthetic as S
+
+    s = S.SETUP
+    f = s["f_abs_test"]
+    om = 2 * np.pi * f
+    N0 = O.pol_tor_angles_2_vector(s["steering_angle_pol"], s["steering_angle_tor"])
+    pos, dirs, w = O.launch_peripheral_rays([s["R0"], 0.0, s["z0"]], N0, s["spot_size"],
+                                            s["inverse_curvature_radius"], f, N_rings=92,
+                                            min_azimuthal_points=11)
+    idx = np.arange(0, len(w), 500)
+    P = T.Plasma(*S.plasma_args(eq))
+    xp, Np, s0, st = T.ray_entry(P, pos[idx], dirs[idx], om, 1)
+    O.abs_al_init(24)
+    r = oplasma.trace(xp, Np, om, 1, 1e-4, 2000, samples=True, traj_stride=1)
+    tau = r["traj"][:, :, 3]
+    alpha = r["samples"][:, 1:, 1] / np.exp(-tau)  # dP/ds_k / P_k
+    a_max = float(np.nanmax(alpha))
+    assert 100.0 < a_max < 1000.0, a_max  # the X2 layer is crossed; the peak is O(500) /m
+    assert a_max * 1e-4 < 0.1
+    z = -a_max * 1e-4
+    assert abs(1 + z + z * z / 2 + z ** 3 / 6 + z ** 4 / 24 - np.exp(z)) < 1e-7
