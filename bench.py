@@ -95,7 +95,15 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # test-only rehearsal of the multi-process path on a one-GPU box: every rank on
+    # device 0 and the reduce over gloo (RCCL refuses two ranks on one device)
+    same_dev = world > 1 and os.environ.get("TORJ_BENCH_SAME_DEVICE") == "1"
+    if same_dev:
+        local = 0
+        dist.init_process_group("gloo")
+    elif world > 1:
+        if local >= torch.cuda.device_count():
+            sys.exit(f"bench.py: LOCAL_RANK {local} but {torch.cuda.device_count()} HIP device(s) visible")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -283,7 +291,9 @@ def main():
                 "n_psi": args.n_psi,
                 "traj_stride": args.traj_stride,
                 "absorption": args.absorption,
-                "parallelism": f"ray-shard x{world} + RCCL all_reduce of dP/dV",
+                "parallelism": (f"ray-shard x{world} on ONE device (TORJ_BENCH_SAME_DEVICE rehearsal, "
+                                f"gloo all_reduce of dP/dV)" if same_dev
+                                else f"ray-shard x{world} + RCCL all_reduce of dP/dV"),
                 "ray_status_counts": {T.STATUS_NAMES[i]: int(c)
                                       for i, c in enumerate(np.bincount(status, minlength=6)) if c},
             },
