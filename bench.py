@@ -338,7 +338,7 @@ def main():
             },
             "work_counters": (
                 {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
-                 "larmor_tests": int(cnt[2]), "faddeeva_evals": int(cnt[3]),
+                 "faddeeva_evals_asymptotic": int(cnt[2]), "faddeeva_evals": int(cnt[3]),
                  "warmdisp_passes": int(cnt[4]), "passes_x_lrm": int(cnt[5]),
                  "sum_lrm": int(cnt[6]), "sum_lrm2": int(cnt[7])}
                 if args.absorption == "warm_wr" else

@@ -217,8 +217,9 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
  *     integrals found exactly zero in calls settled before the polarisation
  *     vector (every harmonic present an exact zero: alpha = 0, no call
  *     reaches the harmonic sum);
- *   absorption 2 (warm, iwarm 1): [2] larmornumber tests, [3] Faddeeva
- *     evaluations, [4] warmdisp passes, [5] passes x Larmor order lrm,
+ *   absorption 2 (warm, iwarm 1): [2] Faddeeva evaluations by the asymptotic
+ *     series (|z| >= 16, of [3]), [3] Faddeeva evaluations, [4] warmdisp
+ *     passes, [5] passes x Larmor order lrm,
  *     [6] sum lrm, [7] sum lrm^2 (one warm alpha per RHS evaluation);
  *   absorption 0 / 3: [2..7] 0.
  * stream: hipStream_t or NULL. */

@@ -20,8 +20,10 @@ dependent parts are counted at their cheapest branch (a lower bound):
   recursion step: the small-|psi| form (1 + phi2 cf1) / (l + 1/2);
   warmdisp: every pass but the last of each call is a full update (the last
   one breaks); unconverged calls (100 updates) are counted with 99.
-The Faddeeva value comes from scipy (its op count from the Weideman form the
-kernel runs, N = 36: a fixed-length complex Horner sum).
+The Faddeeva value comes from scipy; its op count is that of the branch the
+kernel runs (torj_warm.hpp faddeeva_upper): the asymptotic series (10 terms)
+where |x| >= 16 or Im z >= 16, else Weideman's N = 36 complex Horner sum.  The
+model prices larmornumber's resonance tests at one per call (their least).
 """
 from __future__ import annotations
 
@@ -137,20 +139,50 @@ def faddeeva_weideman_count():
 
 
 FAD = faddeeva_weideman_count()
+KFAD_ASYM, KFAD_ASYM_K = 16.0, 10
 
 
-def zetac(x, y):
-    """value from scipy (Z = i sqrt(pi) w), cost FAD"""
+def faddeeva_asym_count():
+    """the kernel's faddeeva_asym + zetac_upper on counting floats (fixed cost)"""
+    c0 = Counter.n
+    x, y = CF(20.0), CF(3.0)
+    ir2 = 1.0 / (x * x + y * y)
+    a, b = x * ir2, -y * ir2
+    ur, ui = 0.5 * (a * a - b * b), a * b
+    tr, ti = CF(1.0), CF(0.0)
+    for j in range(KFAD_ASYM_K - 1, 0, -1):
+        vr, vi = ur * tr - ui * ti, ur * ti + ui * tr
+        tr, ti = (2 * j - 1) * vr + 1.0, (2 * j - 1) * vi
+    pr, pim = a * tr - b * ti, a * ti + b * tr
+    _ = (-0.56 * pim, 0.56 * pr)
+    _ = (-1.77 * _[1], 1.77 * _[0])
+    return Counter.n - c0
+
+
+FAD_ASYM = faddeeva_asym_count()
+
+
+def asym_ok(x, y):
+    """the kernel's branch (torj_warm.hpp faddeeva_asym_ok)"""
+    return abs(float(x)) >= KFAD_ASYM or float(y) >= KFAD_ASYM
+
+
+def zetac(x, y, tr=None):
+    """value from scipy (Z = i sqrt(pi) w), cost of the kernel's branch"""
     from scipy.special import wofz
 
-    Counter.n += FAD
+    asym = asym_ok(x, y)
+    Counter.n += FAD_ASYM if asym else FAD
+    if tr is not None:
+        tr.nfad += 1
+        tr.nasym += int(asym)
     z = 1j * math.sqrt(math.pi) * wofz(complex(float(x), float(y)))
     return CC(z.real, z.imag)
 
 
 class Trips:
     def __init__(self):
-        self.ltrips = self.nfad = self.passes = self.lrm = 0
+        self.ltrips = self.nfad = self.nasym = self.passes = self.lrm = 0
         self.converged = True
 
 
@@ -187,17 +219,14 @@ def fsup_side(sg, isa, inv, tr, state):
     else:
         xp, yp, xm, ym, x0, y0 = psi, phim, -psi, phim, 0.0, phim
     mirror = alpha.v < 0
-    czp = zetac(xp, yp)
-    tr.nfad += 1
+    czp = zetac(xp, yp, tr)
     if mirror:
         czm = CC(-czp.re, czp.im)
     else:
-        czm = zetac(xm, ym)
-        tr.nfad += 1
+        czm = zetac(xm, ym, tr)
     cz0 = None
     if not big:
-        cz0 = zetac(x0, y0)
-        tr.nfad += 1
+        cz0 = zetac(x0, y0, tr)
     cf12 = CC(0.0)
     if alpha.v != 0.0:
         i2phim = 0.5 * (1.0 / phim)
@@ -346,7 +375,7 @@ def alpha_wr(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode):
 def component_counts():
     """per-trip op counts of the model in torj_hip/flops.py, each measured by
     running that piece of alpha_wr's arithmetic on counting floats"""
-    c = {"FLOPS_WARM_FADDEEVA": FAD}
+    c = {"FLOPS_WARM_FADDEEVA": FAD, "FLOPS_WARM_FADDEEVA_ASYM": FAD_ASYM}
     # larmornumber test: ygn, rdu2, gg, mu (gg - 1)
     yg, npl, mu, dnl = CF(0.6), CF(0.1), CF(300.0), CF(0.99)
 
@@ -471,8 +500,9 @@ def model_flops(tr_list, c):
         steps = L * L + 5 * L + 2
         stored = 2 + 6 * L
         upd = tr.passes - 1
-        tot += (c["FLOPS_WARM_CALL"] + tr.ltrips * c["FLOPS_WARM_LARMOR_TEST"]
-                + tr.nfad * c["FLOPS_WARM_FADDEEVA"] + (2 * L + 1) * c["FLOPS_WARM_SIDE"]
+        tot += (c["FLOPS_WARM_CALL"] + 1 * c["FLOPS_WARM_LARMOR_TEST"]
+                + (tr.nfad - tr.nasym) * c["FLOPS_WARM_FADDEEVA"]
+                + tr.nasym * c["FLOPS_WARM_FADDEEVA_ASYM"] + (2 * L + 1) * c["FLOPS_WARM_SIDE"]
                 + steps * c["FLOPS_WARM_STEP"] + stored * c["FLOPS_WARM_STORE"]
                 + (L + 1) * c["FLOPS_WARM_ISA"] + (L * L + 3 * L) // 2 * c["FLOPS_WARM_PAIR"]
                 + L * c["FLOPS_WARM_ORDER"] + tr.passes * L * c["FLOPS_WARM_SUM_TERM"]

@@ -40,7 +40,7 @@ def _points(O, n, seed, mode, te_lo):
 
 def _counters(trs):
     """the kernel's counters [1..7] from restatement trips"""
-    return [len(trs), sum(t.ltrips for t in trs), sum(t.nfad for t in trs),
+    return [len(trs), sum(t.nasym for t in trs), sum(t.nfad for t in trs),
             sum(t.passes for t in trs), sum(t.passes * t.lrm for t in trs),
             sum(t.lrm for t in trs), sum(t.lrm * t.lrm for t in trs)]
 
@@ -66,7 +66,10 @@ def test_restatement_values_and_model_bound(O, FW, mode):
             trs.append(tr)
             count += c
             m = FW.model_flops([tr], FW.component_counts())
-            assert 0.97 * c <= m <= c, (pt, m, c)
+            # per point: larmornumber's tests are priced at one per call (the
+            # counter slot carries the asymptotic Faddeeva evaluations), so a
+            # cheap point with many resonance tests sits a few % low
+            assert 0.94 * c <= m <= c, (pt, m, c)
     assert len(trs) > 90
     assert max(errs) <= 1e-7, max(errs)
     # flops.py's aggregate form (minus the cold RHS it adds per call) = the sum

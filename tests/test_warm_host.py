@@ -46,6 +46,44 @@ def test_zetac_matches_wofz(H, box):
     assert (np.abs(z - ref)[fin] / np.abs(ref)[fin]).max() <= 1e-13
 
 
+def test_zetac_asymptotic_branch_vs_mpmath(H):
+    """|x| >= 16 or Im z >= 16: the asymptotic series (torj_warm.hpp
+    faddeeva_asym, 10 terms) against mpmath's w(z) = exp(-z^2) erfc(-iz) at 30
+    digits, across the upper half plane and |z| up to 1.6e4: 2e-15 of |Z|, and
+    the real part (the absorption) to the same relative accuracy wherever it is
+    above 1e-30 of |Z| (on the real axis it is exp(-x^2), to the rounding).  Both sides
+    of the branch boundary agree to the Weideman branch's 1e-13."""
+    import mpmath as mp
+
+    rng = np.random.default_rng(5)
+    n = 1500
+    r = 16.0 * np.exp(rng.uniform(0.0, np.log(1e3), n))
+    th = np.where(rng.random(n) < 0.25, 0.0, rng.uniform(0.0, np.pi, n))
+    x, y = r * np.cos(th), r * np.sin(th)
+    keep = (np.abs(x) >= 16.0) | (y >= 16.0)
+    x, y = x[keep], y[keep]
+    m = len(x)
+    out = np.zeros(2 * m)
+    H.wh_zetac(m, _d(x), _d(y), _d(out))
+    z = out[0::2] + 1j * out[1::2]
+    with mp.workdps(30):
+        ref = np.array([complex(1j * mp.sqrt(mp.pi) * mp.exp(-mp.mpc(a, b) ** 2) * mp.erfc(-1j * mp.mpc(a, b)))
+                        for a, b in zip(x, y)])
+    assert (np.abs(z - ref) / np.abs(ref)).max() <= 2e-15
+    im = np.abs(ref.imag) > 1e-30 * np.abs(ref)  # Im Z = sqrt(pi) Re w
+    assert (np.abs(z.imag - ref.imag)[im] / np.abs(ref.imag)[im]).max() <= 2e-15
+    ax = y == 0.0
+    ex = math.sqrt(math.pi) * np.exp(-x[ax] ** 2)
+    assert ax.sum() > 100 and np.all(np.abs(z.imag[ax] - ex) <= 1e-15 * ex)
+    # the branch boundary |x| = 16 (y < 16): both sides continuous to 1e-13
+    xb = np.array([np.nextafter(16.0, 0.0), 16.0, -np.nextafter(16.0, 0.0), -16.0])
+    for yb in (0.0, 1e-3, 0.5, 5.0, 15.9):
+        o = np.zeros(8)
+        H.wh_zetac(4, _d(xb), _d(np.full(4, yb)), _d(o))
+        zz = o[0::2] + 1j * o[1::2]
+        assert abs(zz[0] - zz[1]) <= 1e-13 * abs(zz[1]) and abs(zz[2] - zz[3]) <= 1e-13 * abs(zz[3])
+
+
 def test_expei_matches_expi(H):
     rng = np.random.default_rng(2)
     x = np.concatenate([10 ** rng.uniform(-8, 2.8, 20000), -(10 ** rng.uniform(-8, 2.8, 20000))])

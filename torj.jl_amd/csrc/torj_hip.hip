@@ -1140,7 +1140,7 @@ __global__ void __launch_bounds__(256, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TOR
                                             in[5 * (size_t)a.n], a.mode);
     sp.alpha[(size_t)js * a.n + i] = r.alpha;
     if (sp.awork)
-        sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.ltrips, 127) | ((unsigned)min(r.nfad, 127) << 7) |
+        sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.nasym, 127) | ((unsigned)min(r.nfad, 127) << 7) |
                                      ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
 }
 

@@ -357,14 +357,50 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
     }
     return {u, v};
 }
+// w(z) for Im z >= 0 with |x| >= 16 or y >= 16 (so |z| >= 16): the asymptotic
+// series w(z) ~ i / (sqrt(pi) z) sum_{k < 10} (2k-1)!! / (2 z^2)^k, nested as
+// 1 + u (1 + 3 u (1 + 5 u (...))), u = 1 / (2 z^2); its 10th term is below 2e-17
+// of the first there.  Against mpmath's w over |z| in [16, 1.6e4] across the
+// upper half plane: 4.5e-16 relative, Re w included wherever it exceeds 1e-30
+// |w| (Weideman: 2.5e-14; tests/test_warm_host.py).  On the real axis Re w =
+// exp(-x^2) is set exactly, as in the Weideman branch; just above the axis the
+// series omits the exponentially small Stokes term (<= exp(1 - x^2) |w| ~ 1e-111
+// |w| for y < 1 at |x| >= 16), which Weideman's absolute error does not resolve
+// either.  It serves ~90 % of the C5 beam's evaluations (median |z| ~ 40) at
+// about half the Weideman cost: C5 trace phase 162.1 -> 143.8 ms.
+constexpr double kFadAsym = 16.0;
+constexpr int kFadAsymK = 10;
+TORJ_HD bool faddeeva_asym_ok(double x, double y) { return fabs(x) >= kFadAsym || y >= kFadAsym; }
+TORJ_HD cplx faddeeva_asym(double x, double y) {
+    constexpr double kInvSqrtPi = 0.56418958354775628695;
+    const double ir2 = rcp_nz(fma(x, x, y * y));
+    const double a = x * ir2, b = -y * ir2;  // 1 / z
+    const double ur = 0.5 * fma(a, a, -b * b), ui = a * b;  // u = (1 / z)^2 / 2
+    double tr = 1.0, ti = 0.0;
+#pragma unroll
+    for (int j = kFadAsymK - 1; j >= 1; j--) {  // T = 1 + (2j - 1) u T
+        const double vr = fma(ur, tr, -ui * ti), vi = fma(ur, ti, ui * tr);
+        tr = fma((double)(2 * j - 1), vr, 1.0);
+        ti = (double)(2 * j - 1) * vi;
+    }
+    const double pr = fma(a, tr, -b * ti), pim = fma(a, ti, b * tr);  // T / z
+    cplx w;
+    w.re = -kInvSqrtPi * pim;  // i T / (sqrt(pi) z)
+    w.im = kInvSqrtPi * pr;
+    if (y == 0.0) w.re = exp(-x * x);
+    return w;
+}
+
 // w(z) for Im z >= 0 by Weideman's rational approximation (N = 36,
 // tools/gen_faddeeva_coefs.py; 2.5e-14 relative to scipy's wofz): a fixed-cost
 // complex Horner sum with no branches, where TOMS 680 picks a series or a
 // continued fraction of data-dependent length per argument -- divergent across
 // a wave.  On the real axis Re w = exp(-x^2) exactly (as TOMS 680 sets it:
 // the absorption is that term).
+// (|z| < 16; faddeeva_asym above).
 TORJ_HD cplx faddeeva_upper(double x, double y) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
+    if (faddeeva_asym_ok(x, y)) return faddeeva_asym(x, y);
     const double dr = kWeidL + y, di = -x;  // D = L - iz, Re D >= L > 0
     const double id = rcp_nz(fma(dr, dr, di * di));
     const double ir = dr * id, ii = -di * id;  // 1 / D
@@ -391,6 +427,12 @@ TORJ_HD cplx faddeeva_upper(double x, double y) {
 // other issue slot empty
 TORJ_HD void faddeeva_upper2(double x0, double y0, double x1, double y1, cplx &w0, cplx &w1) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
+    const bool a0 = faddeeva_asym_ok(x0, y0), a1 = faddeeva_asym_ok(x1, y1);
+    if (a0 || a1) {  // the same branches as faddeeva_upper, so the same bits
+        w0 = a0 ? faddeeva_asym(x0, y0) : faddeeva_upper(x0, y0);
+        w1 = a1 ? faddeeva_asym(x1, y1) : faddeeva_upper(x1, y1);
+        return;
+    }
     const double xs[2] = {x0, x1}, ys[2] = {y0, y1};
     double ir[2], ii[2], Zr[2], Zi[2], pr[2], pim[2];
 #pragma unroll
@@ -502,12 +544,18 @@ TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx 
         for (int q = 0; q < 2; q++)
             cz[q][1] = mirror[q] ? C(-cz[q][0].re, cz[q][0].im) : zetac_upper(zx[q][1], zy[q][1]);
     }
-    int nfad = 0;  // Faddeeva evaluations of the reference's algorithm (the work counters, torj_hip/flops.py)
+    // Faddeeva evaluations of the reference's algorithm and those of them the
+    // asymptotic series serves (the work counters, torj_hip/flops.py), packed
+    // as nfad | nasym << 16
+    int nfad = 0;
 #pragma unroll
     for (int q = 0; q < 2; q++) {
         if (q == 0 && isa == 0) continue;
         const int is = q == 0 ? -isa : isa;
         nfad += (big_psi ? 2 : 3) - (mirror[q] ? 1 : 0);
+        nfad += (faddeeva_asym_ok(zx[q][0], zy[q][0]) + (!mirror[q] && faddeeva_asym_ok(zx[q][1], zy[q][1])) +
+                 (!big_psi && faddeeva_asym_ok(zx[q][2], zy[q][2])))
+                << 16;
         const cplx czp = cz[q][0], czm = cz[q][1], cz0 = cz[q][2];
         cplx cf12 = C(0.0);
         if (alpha[q] != 0.0) {
@@ -839,6 +887,7 @@ struct WarmAlpha {
     // trip counts of the data-dependent loops (iwarm 1: Faddeeva evaluations;
     // both: warmdisp passes, Larmor order, larmornumber tests) -> torj_hip/flops.py
     int nfad, passes, lrm, ltrips;
+    int nasym;  // of the nfad, those by the asymptotic series (faddeeva_asym)
 };
 template <int IWARM, int L>
 TORJ_HD WarmAlpha alpha_core(double omega, double X, double Y, double N_par, double mu, double npr,
@@ -854,7 +903,7 @@ TORJ_HD WarmAlpha alpha_core(double omega, double X, double Y, double N_par, dou
     T.e[0][2] = T.e[0][2] + 1.0;
     const int sox = Y <= 1.0 ? mode : -mode;
     const cplx a2 = warmdisp_n2<L>(X, Y, N_par, npr, sox, lrm, T, passes);
-    return {2.0 * a2.im * omega / kC * inv_dDdN, a2, nfad, passes, lrm, 0};
+    return {2.0 * a2.im * omega / kC * inv_dDdN, a2, nfad & 0xffff, passes, lrm, 0, nfad >> 16};
 }
 
 // The tensor is sized for lrm <= 3 (the common case: one to three Larmor
@@ -915,7 +964,7 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
             alpha_warm_v<ABS == 2 ? 1 : 3>(omega, p.X, p.Y, Nabs, Npar, exp(p.lnTe), inv, mode);
         alpha = r.alpha;
         if (ABS == 2 && work) {  // the weakly relativistic op count's trips (flops.py)
-            work->n_active += r.ltrips;
+            work->n_active += r.nasym;
             work->n_harm += r.nfad;
             work->n_terms += r.passes;
             work->n_zero += r.passes * r.lrm;

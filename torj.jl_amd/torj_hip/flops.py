@@ -78,7 +78,8 @@ def algorithmic_flops_reference(counters, n_gl: int = 24) -> float:
 # 99.8 % of the instrumented count, tests/test_warm_flops.py).
 FLOPS_WARM_CALL = 77          # Te, |N|, mu, N_perp, per-call invariants, e330, alpha
 FLOPS_WARM_LARMOR_TEST = 10   # per larmornumber resonance test
-FLOPS_WARM_FADDEEVA = 278     # per Z(z): Weideman N = 36 complex Horner sum
+FLOPS_WARM_FADDEEVA = 278     # per Z(z) by Weideman's N = 36 complex Horner sum (|z| < 16)
+FLOPS_WARM_FADDEEVA_ASYM = 102  # per Z(z) by the asymptotic series (|x| or Im z >= 16), 10 terms
 FLOPS_WARM_SIDE = 14          # per fsup side s = +-|s|: alpha_s, phi, cf12, cf32
 FLOPS_WARM_STEP = 6           # per Shkarofsky recursion step
 FLOPS_WARM_STORE = 4          # per stored recursion step: cefp, cefm accumulation
@@ -91,16 +92,20 @@ FLOPS_WARM_UPDATE = 168       # per warmdisp update: cc4, cc2, cc0, root, conver
 
 def algorithmic_flops_warm(counters) -> float:
     """counters = the 8 work counters of an absorption-2 launch (include/torj_hip.h
-    torj_trace_device): ray-steps, RHS evaluations (= warm alpha calls), larmornumber
-    tests, Faddeeva evaluations, warmdisp passes, passes x lrm, sum lrm, sum lrm^2."""
-    steps, calls, tests, fad, passes, pass_l, sl, sl2 = (float(c) for c in counters[:8])
+    torj_trace_device): ray-steps, RHS evaluations (= warm alpha calls), Faddeeva
+    evaluations by the asymptotic series, Faddeeva evaluations (all), warmdisp
+    passes, passes x lrm, sum lrm, sum lrm^2.  larmornumber's resonance tests are
+    priced at one per call (their least; a lower bound)."""
+    steps, calls, asym, fad, passes, pass_l, sl, sl2 = (float(c) for c in counters[:8])
+    tests = calls
     sides = 2.0 * sl + calls                  # is = -|s| .. |s|
     rsteps = sl2 + 5.0 * sl + 2.0 * calls     # recursion steps: lrm^2 + 5 lrm + 2 per call
     stored = 6.0 * sl + 2.0 * calls
     pairs = 0.5 * (sl2 + 3.0 * sl)            # (|s|, l), max(|s|, 1) <= l <= lrm
     updates = passes - calls                  # every pass but the breaking one
     return (steps * FLOPS_STEP_OVERHEAD + calls * (FLOPS_RHS_COLD + FLOPS_WARM_CALL)
-            + tests * FLOPS_WARM_LARMOR_TEST + fad * FLOPS_WARM_FADDEEVA
+            + tests * FLOPS_WARM_LARMOR_TEST + (fad - asym) * FLOPS_WARM_FADDEEVA
+            + asym * FLOPS_WARM_FADDEEVA_ASYM
             + sides * FLOPS_WARM_SIDE + rsteps * FLOPS_WARM_STEP + stored * FLOPS_WARM_STORE
             + (sl + calls) * FLOPS_WARM_ISA + pairs * FLOPS_WARM_PAIR + sl * FLOPS_WARM_ORDER
             + pass_l * FLOPS_WARM_SUM_TERM + updates * FLOPS_WARM_UPDATE)
