@@ -1091,6 +1091,11 @@ __global__ void __launch_bounds__(512, TORJ_TRAJ_LDS_WAVES) k_traj_lds(TraceArgs
 // (a measured alternative -- harmonic 2 in a second pass over a compacted list
 // of the points needing it -- executed more instructions in total: the points
 // needing harmonic 2 cluster in whole waves)
+// COUNT: a counted launch (sp.awork set) -- the work words are written; an
+// uncounted one carries no work struct at all (with its address taken
+// conditionally it lived in scratch: 32 B of stores per lane and point, ~25 GB
+// per headline launch)
+template <bool COUNT>
 __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
     const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
     const int i = q * 256 + threadIdx.x;
@@ -1102,15 +1107,19 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     // alpha the scan never reads
     if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
     const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
-    AlbajarWork work = {};
-    const double al = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-        c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
-        in[4 * (size_t)a.n], a.mode, sp.awork ? &work : nullptr);
-    sp.alpha[(size_t)js * a.n + i] = al;
-    if (sp.awork)  // a counted launch (null otherwise: no work words written or read)
+    if constexpr (COUNT) {
+        AlbajarWork work = {};
+        sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
+            c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
+            in[4 * (size_t)a.n], a.mode, &work);
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
                                      ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
+    } else {
+        sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
+            c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
+            in[4 * (size_t)a.n], a.mode, nullptr);
+    }
 }
 
 // the warm alpha (absorption 2 / 3, iwarm 1 / 3) at the stored stage points:
@@ -2520,8 +2529,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             hipLaunchKernelGGL(k_alpha_warm_pts<3>, agrid, dim3(256), 0, s2, a, sp, nq);
         else if (a.abs_model == 2)
             hipLaunchKernelGGL(k_alpha_warm_pts<1>, agrid, dim3(256), 0, s2, a, sp, nq);
+        else if (sp.awork)  // a counted launch
+            hipLaunchKernelGGL(k_alpha_pts<true>, agrid, dim3(256), 0, s2, a, sp, nq);
         else
-            hipLaunchKernelGGL(k_alpha_pts, agrid, dim3(256), 0, s2, a, sp, nq);
+            hipLaunchKernelGGL(k_alpha_pts<false>, agrid, dim3(256), 0, s2, a, sp, nq);
         HIPCK(hipEventRecord(p->ev_A[r], s2));
         if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_A[r], 0));
         TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s3, a, sp);
