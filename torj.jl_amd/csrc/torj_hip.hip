@@ -1167,8 +1167,11 @@ __device__ void cold_replay(const TraceArgs &a, double x[3], double N[3], int k)
     }
 }
 
-template <int DEPO, bool TRAJ>
-__global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
+// COUNT: a counted launch (work words and counters); the uncounted scan
+// carries neither the accumulators nor their loads (fewer registers beside the
+// alpha waves it shares the SIMDs with)
+template <int DEPO, bool TRAJ, bool COUNT>
+__device__ __forceinline__ void tau_scan_body(const TraceArgs &a, const SplitArgs &sp) {
     const int i = blockIdx.x * 64 + threadIdx.x;
     // counters [2..7] (include/torj_hip.h): Albajar or warm iwarm 1 meanings
     unsigned long long nsteps = 0, c2 = 0, c3 = 0, c4 = 0, c5 = 0, c6 = 0, c7 = 0;
@@ -1210,7 +1213,7 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
                     break;
                 }
 #pragma unroll
-                for (int q = 0; q < 4 && sp.awork; q++) {
+                for (int q = 0; q < 4 && COUNT; q++) {
                     const unsigned wk = sp.awork[o + q * (size_t)a.n];
                     if (am == 1) {
                         c2 += wk & 1u;
@@ -1263,7 +1266,7 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
             sp.sinfo[i] = make_info(steps, st);
         }
     }
-    if (a.counters) {
+    if (COUNT) {
         const unsigned long long s0 = wave_sum(nsteps), s2 = wave_sum(c2), s3 = wave_sum(c3),
                                  s4 = wave_sum(c4), s5 = wave_sum(c5), s6 = wave_sum(c6),
                                  s7 = wave_sum(c7);
@@ -1278,6 +1281,14 @@ __global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
             atomicAdd(a.counters + 7, s7);
         }
     }
+}
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64) k_tau_scan(TraceArgs a, SplitArgs sp) {
+    tau_scan_body<DEPO, TRAJ, false>(a, sp);
+}
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64) k_tau_scan_counted(TraceArgs a, SplitArgs sp) {
+    tau_scan_body<DEPO, TRAJ, true>(a, sp);
 }
 
 // final state, status and steps; trajectory samples past an earlier scan stop
@@ -2535,7 +2546,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             hipLaunchKernelGGL(k_alpha_pts<false>, agrid, dim3(256), 0, s2, a, sp, nq);
         HIPCK(hipEventRecord(p->ev_A[r], s2));
         if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_A[r], 0));
-        TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s3, a, sp);
+        if (a.counters)
+            TORJ_SPLIT_DISPATCH(k_tau_scan_counted, dim3(G), dim3(64), 0, s3, a, sp);
+        else
+            TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s3, a, sp);
         HIPCK(hipEventRecord(p->ev_S[r], s3));
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
