@@ -1,5 +1,5 @@
 """Prints the GPU-vs-oracle error of abs_Albajar_fast on the random physical
-sweep of tests/test_gpu_parity.py (the node loop's exp_node / sqrt_node)."""
+sweep of tests/test_gpu_parity.py (the node loop's exp2_node / sqrt_node)."""
 import json
 import os
 import sys

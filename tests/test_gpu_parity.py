@@ -125,7 +125,7 @@ def albajar_random_sweep(T, O, n=20000, seed=7):
 
 
 def test_albajar_random_physical_sweep(gpu, T, O):
-    """The node loop's exp_node / sqrt_node (torj_math.hpp) keep alpha within the
+    """The node loop's exp2_node / sqrt_node (torj_math.hpp) keep alpha within the
     1e-10 parity bar of the libm oracle on 20 000 random physical inputs."""
     rel, ab, _ = albajar_random_sweep(T, O)
     assert len(rel) > 5000  # most tuples absorb

@@ -1,5 +1,5 @@
 """Coefficients of the device exp polynomials (torj_math.hpp exp_fast: degree
-11; exp_node, the Albajar node loop: degree 9 -- `python tools/gen_exp_poly.py 9`).
+11; exp2_node, the Albajar node loop: degree 9, coefficients scaled by ln2^i -- `python tools/gen_exp_poly.py 9 --base2`).
 
 e^r on |r| <= ln2/2 as 1 + r + r^2 q(r), q of degree 9 interpolated at its
 Chebyshev nodes in 50-digit arithmetic (near-minimax): degree 11 overall, max
@@ -34,7 +34,10 @@ def max_ulp(co):
 
 if __name__ == "__main__":
     import sys
-    co = fit(int(sys.argv[1]) if len(sys.argv) > 1 else 11)
+    co = fit(int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 11)
     print("max error %.2f ulp" % max_ulp(co))
     for k, v in enumerate(co):
         print(f"c{k} = {v!r}")
+    if "--base2" in sys.argv:  # exp2_node: 2^r = e^(r ln2) on |r| <= 1/2, d_k = c_k ln2^k
+        for k, v in enumerate(co):
+            print(f"d{k} = {float(mpf(v) * log(2) ** k)!r}")

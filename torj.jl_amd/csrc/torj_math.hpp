@@ -122,7 +122,7 @@ TORJ_HD double sqrt_nn(double x) {
 // exp(mu (1 - gamma)) with mu (gamma - 1) < 760 on every node that is not an
 // exact zero, so a relative error e moves a node term by ~mu gamma e; the
 // Albajar golden sweep and the headline-fan parity hold at 1e-10 (C3 trace
-// phase -2.5 % on top of exp_node).
+// phase -2.5 % on top of the degree-9 node exp).
 TORJ_HD double sqrt_node(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double y = __builtin_amdgcn_rsq(x);
@@ -136,7 +136,7 @@ TORJ_HD double sqrt_node(double x) {
 // exp on the device: range reduction + degree-11 near-minimax polynomial +
 // ldexp (~1 ulp).  No special-case paths: ldexp overflows to inf above ~709
 // and underflows to 0 below ~-745, NaN stays NaN.  Used for n_e, T_e from
-// their log splines (the node loop takes exp_node below).
+// their log splines (the node loop takes exp2_node below).
 TORJ_HD double exp_fast(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double k = __builtin_rint(x * 1.4426950408889634074);
@@ -166,32 +166,37 @@ TORJ_HD double exp_fast(double x) {
 #endif
 }
 
-// exp of the Albajar node loop, exp(mu (1 - gamma)): the same range reduction
-// with a degree-9 near-minimax polynomial (tools/gen_exp_poly.py 9: 333 ulp,
-// 7.4e-14 relative).  Each node term carries it once; the harmonic sum stays
-// within ~1e-13 of the libm one, three orders under the 1e-10 parity bar, and
-// the two fma saved per exp are 4 of the pair's ~100 VALU instructions
-// (C3 trace phase -1.8 %).
-TORJ_HD double exp_node(double x) {
+// exp of the Albajar node loop, exp(mu (1 - gamma)), in base 2: exp2_node(y) =
+// 2^y with y = mu log2(e) (1 - gamma) formed by the caller (mu log2(e) is a
+// per-harmonic constant, so y costs the one fma the natural exponent did).
+// k = round(y) by the 1.5 * 2^52 shifter (k in the low word of kd: no v_rndne,
+// no v_cvt), r = y - k exact (Sterbenz, |r| <= 1/2), and a degree-9
+// near-minimax polynomial for 2^r: exp's on |x| <= ln2/2 (tools/gen_exp_poly.py
+// 9: 333 ulp, 7.4e-14 relative) with its coefficients scaled by ln2^i.  Each
+// node term carries it once; the harmonic sum stays within ~1e-13 of the libm
+// one, three orders under the 1e-10 parity bar.  13 VALU against exp_fast's
+// 17: 3 for the reduction instead of 5, degree 9 instead of 11.  Exact for |y| < 2^51;
+// node arguments have mu = m_e c^2 / Te < 25 550 (Te >= 20 eV,
+// src/absorption.jl:194).  Every node of a lane the exact-zero bound skips has
+// y < -1096 and gives exactly +0, so the skip stays bit-identical.
+TORJ_HD double exp2_node(double y) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const double k = __builtin_rint(x * 1.4426950408889634074);
-    double r = fma(-k, 6.93147180559945286227e-01, x);
-    r = fma(-k, 2.31904681384629955842e-17, r);
-    double p = 2.7617564785876086e-06;
-    p = fma(p, r, 2.4867870179687727e-05);
-    p = fma(p, r, 0.00019841224599656011);
-    p = fma(p, r, 0.0013888839110572009);
-    p = fma(p, r, 0.00833333334420298);
-    p = fma(p, r, 0.04166666678626573);
-    p = fma(p, r, 0.16666666666662586);
-    p = fma(p, r, 0.4999999999995511);
+    const double kd = y + 0x1.8p52;
+    const double r = y - (kd - 0x1.8p52);
+    double p = 1.0200337248760112e-07;
+    p = fma(p, r, 1.325080551750225e-06);
+    p = fma(p, r, 1.5252699025121892e-05);
+    p = fma(p, r, 0.00015403475186530786);
+    p = fma(p, r, 0.0013333558163820172);
+    p = fma(p, r, 0.00961812913523614);
+    p = fma(p, r, 0.05550410866480799);
+    p = fma(p, r, 0.24022650695888503);
+    p = fma(p, r, 0.6931471805599453);
     p = fma(p, r, 1.0);
-    p = fma(p, r, 1.0);
-    int ki;
-    asm("v_cvt_i32_f64 %0, %1" : "=v"(ki) : "v"(k));
+    const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, kd);  // k, low word
     return __builtin_amdgcn_ldexp(p, ki);
 #else
-    return exp(x);
+    return exp2(y);
 #endif
 }
 
@@ -549,6 +554,7 @@ TORJ_HD void series_pair_loop(double z, double &Sa, double &Sb) {
 // Per-harmonic constants of the node sum (abs_Al_pol_fact / abs_Al_integral_nume_fast)
 struct HarmConst {
     double x_m, K0, K1, K2, K3, K4, K5, upa0, upa1, r2m1, mu;
+    double mu2;  // mu log2(e): the node exponent in base 2 (exp2_node)
     // node-pair form: gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
     double C0, C1, C2, hx;
 };
@@ -634,11 +640,11 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double P = fma(A, fma(c.K3, t2, c.K0), fma(Cc, c.K1, -B));
     const double wp = w * p;
     const double a = fma(c.C1, t2, c.C0);
-    if (single) return wp * P * exp_node(fma(-c.mu, sqrt_node(a), c.mu));
+    if (single) return wp * P * exp2_node(fma(-c.mu2, sqrt_node(a), c.mu2));
     const double Q = fma(A, c.K4, Cc * c.K5);
     const double b = c.C2 * t;
-    const double Ep = exp_node(fma(-c.mu, sqrt_node(a + b), c.mu));
-    const double Em = exp_node(fma(-c.mu, sqrt_node(a - b), c.mu));
+    const double Ep = exp2_node(fma(-c.mu2, sqrt_node(a + b), c.mu2));
+    const double Em = exp2_node(fma(-c.mu2, sqrt_node(a - b), c.mu2));
     return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 
@@ -803,6 +809,7 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     c.upa0 = hg.upa0;
     c.upa1 = hg.upa1;
     c.mu = mu;
+    c.mu2 = mu * 1.4426950408889634074;
     c.C0 = hg.C0;
     c.C1 = hg.C1;
     c.C2 = hg.C2;
