@@ -367,14 +367,20 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
     return r;
 }
 
-// Plasma parameters at a point, with Cartesian gradients (eval_plasma,
-// src/dispersion.jl:7-15; B_spline/n_e/T_e, src/plasma.jl:73-89).
+// Plasma parameters at a point (eval_plasma, src/dispersion.jl:7-15;
+// B_spline/n_e/T_e, src/plasma.jl:73-89), with the spatial derivatives the ray
+// RHS needs kept in cylindrical form: the fields depend on (R, Z) only, so
+// d/dx = c d/dR, d/dy = s d/dR, d/dz = d/dZ, and the rotation of B's
+// components adds one tangential term (dispersion_grad).
 struct PlasmaPoint {
     double X, Y, b[3], Babs, invB, B[3], ne;
     double lnTe, psi;
-    // gradients wrt x (Cartesian)
-    double dX[3], dY[3];
-    double dB[3][3];  // dB[k][c] = dB_c / dx_k
+    double c, s, invR;         // x = R (c, s), 1 / R
+    double Bc[3];              // (B_R, B_phi, B_Z)
+    double dBR[3], dBZ[3];     // d/dR, d/dZ of (B_R, B_phi, B_Z)
+    double dBabsR, dBabsZ;     // d|B|/dR, d|B|/dZ
+    double dlnR, dlnZ;         // d ln ne / dR, d ln ne / dZ
+    double Cy;                 // Y = |B| Cy
 };
 
 struct Consts {
@@ -416,17 +422,17 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     }
     const double Br = f.v[0], Bp = f.v[1], Bz = f.v[2];
     const double Bx = Br * c - Bp * s, By = Br * s + Bp * c;
-    const double BxR = f.dR[0] * c - f.dR[1] * s, ByR = f.dR[0] * s + f.dR[1] * c;
-    // d/dx, d/dy, d/dz of (Bx, By, Bz): rotation of the cylindrical components
-    p.dB[0][0] = BxR * c + s * By * invR;
-    p.dB[0][1] = ByR * c - s * Bx * invR;
-    p.dB[0][2] = f.dR[2] * c;
-    p.dB[1][0] = BxR * s - c * By * invR;
-    p.dB[1][1] = ByR * s + c * Bx * invR;
-    p.dB[1][2] = f.dR[2] * s;
-    p.dB[2][0] = f.dZ[0] * c - f.dZ[1] * s;
-    p.dB[2][1] = f.dZ[0] * s + f.dZ[1] * c;
-    p.dB[2][2] = f.dZ[2];
+    p.c = c;
+    p.s = s;
+    p.invR = invR;
+    p.Bc[0] = Br;
+    p.Bc[1] = Bp;
+    p.Bc[2] = Bz;
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        p.dBR[q] = f.dR[q];
+        p.dBZ[q] = f.dZ[q];
+    }
     p.B[0] = Bx;
     p.B[1] = By;
     p.B[2] = Bz;
@@ -441,32 +447,45 @@ TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const 
     p.ne = ne;
     p.X = ne * k.Cx;
     p.Y = Babs * k.Cy;
-    const double dlnne[3] = {f.dR[3] * c, f.dR[3] * s, f.dZ[3]};
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        p.dX[q] = p.X * dlnne[q];
-        p.dY[q] = k.Cy * (p.b[0] * p.dB[q][0] + p.b[1] * p.dB[q][1] + p.b[2] * p.dB[q][2]);
-    }
+    p.Cy = k.Cy;
+    p.dlnR = f.dR[3];
+    p.dlnZ = f.dZ[3];
+    // d|B| = (B_cyl . dB_cyl) / |B|: |B| is axisymmetric (no tangential term)
+    p.dBabsR = (Br * f.dR[0] + Bp * f.dR[1] + Bz * f.dR[2]) * invB;
+    p.dBabsZ = (Br * f.dZ[0] + Bp * f.dZ[1] + Bz * f.dZ[2]) * invB;
 }
 
 // D(x,N) and its gradients (replaces ForwardDiff in gradΛ!, src/solve.jl:85-93).
 // du = (dD/dN, -dD/dx) / |dD/dN|.
+//
+// dD/dx = -(dN_s^2/dX dX/dx + dN_s^2/dY dY/dx + dN_s^2/dN_par dN_par/dx) in
+// cylindrical form.  X and Y depend on (R, Z) only; N_par = N . B / |B| with N
+// held fixed, N . B = N_R B_R + N_phi B_phi + N_Z B_Z where N_R = N_x c + N_y s,
+// N_phi = N_y c - N_x s turn with the point: d(N . B)/dx = c G_R + s W,
+// d(N . B)/dy = s G_R - c W, d(N . B)/dz = G_Z, with G_R, G_Z the contractions
+// of (N_R, N_phi, N_Z) with d/dR, d/dZ of (B_R, B_phi, B_Z) and
+// W = (N_R B_phi - N_phi B_R) / R.  So every x-gradient is (c A_R + s A_W,
+// s A_R - c A_W, A_Z): ~30 VALU per RHS fewer than the rotated 3 x 3 Jacobian.
 TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode, double du[6],
                                double *Npar_out, double *inv_out = nullptr) {
     const double Npar = N[0] * p.b[0] + N[1] * p.b[1] + N[2] * p.b[2];
     const NsPartials ns = refractive_index_sq_partials(p.X, p.Y, Npar, mode);
     const double N2 = N[0] * N[0] + N[1] * N[1] + N[2] * N[2];
-    double dDdN[3], dDdx[3];
+    double dDdN[3];
 #pragma unroll
     for (int q = 0; q < 3; q++) dDdN[q] = 2.0 * N[q] - ns.dNp * p.b[q];
     const double invB = p.invB;
-#pragma unroll
-    for (int q = 0; q < 3; q++) {
-        const double NdB = N[0] * p.dB[q][0] + N[1] * p.dB[q][1] + N[2] * p.dB[q][2];
-        const double bdB = p.b[0] * p.dB[q][0] + p.b[1] * p.dB[q][1] + p.b[2] * p.dB[q][2];
-        const double dNpar = (NdB - Npar * bdB) * invB;
-        dDdx[q] = -(ns.dX * p.dX[q] + ns.dY * p.dY[q] + ns.dNp * dNpar);
-    }
+    const double NR = N[0] * p.c + N[1] * p.s, NP = N[1] * p.c - N[0] * p.s;
+    const double GR = NR * p.dBR[0] + NP * p.dBR[1] + N[2] * p.dBR[2];
+    const double GZ = NR * p.dBZ[0] + NP * p.dBZ[1] + N[2] * p.dBZ[2];
+    const double W = (NR * p.Bc[1] - NP * p.Bc[0]) * (p.invR * invB);
+    // dN_par = (d(N . B) - N_par d|B|) / |B| (radial, vertical; tangential W)
+    const double UR = (GR - Npar * p.dBabsR) * invB, UZ = (GZ - Npar * p.dBabsZ) * invB;
+    const double gX = ns.dX * p.X, gY = ns.dY * p.Cy;
+    const double DR = gX * p.dlnR + gY * p.dBabsR + ns.dNp * UR;
+    const double DZ = gX * p.dlnZ + gY * p.dBabsZ + ns.dNp * UZ;
+    const double DW = ns.dNp * W;
+    const double dDdx[3] = {-(p.c * DR + p.s * DW), -(p.s * DR - p.c * DW), -DZ};
     const double nrm = sqrt_pos(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
     const double inv = rcp_nz(nrm);
     if (inv_out) *inv_out = inv;
@@ -478,6 +497,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
     if (Npar_out) *Npar_out = Npar;
     return N2 - ns.Ns2;
 }
+
 
 // ---------------------------------------------------------------------------
 // Albajar absorption, src/absorption.jl:10-64, 132-226
