@@ -128,4 +128,49 @@ void fd_profile(int n, int n_steps, int n_psi, double ds, const double *grid, co
     for (size_t k = 0; k + 1 < L; k++)
         for (size_t i = 0; i < N; i++) dPs[k * N + i] = dp[k * N + i];
 }
+
+// the streamed deposition of the split pipeline (k_depo_stream after each
+// scan, k_depo_tail after the trace) on the host: the scan's steps S grow by
+// `inc` per emulated block while the ray runs (S < steps[i]), then the tail
+void fd_profile_stream(int n, int n_steps, int n_psi, double ds, const double *grid, const double *s0,
+                       const int *steps, const double *psiL, const double *smp_psi,
+                       const double *smp_dpds, int inc, double *dPs, int *kstar, double *Pray) {
+    const size_t K = (size_t)n_steps + 2, N = (size_t)n, L = (size_t)n_psi, KN = torj::smp_elems(N, K);
+    std::vector<double> E(KN), G1(KN), G2(KN), Fo(L * N, NAN), dp(L * N, 0.0);
+    std::vector<double> sp(KN), sd(KN);
+    for (size_t j = 0; j <= (size_t)n_steps; j++)
+        for (size_t i = 0; i < N; i++) {
+            sp[torj::smp_at(j, (int)i, K)] = smp_psi[j * N + i];
+            sd[torj::smp_at(j, (int)i, K)] = smp_dpds[j * N + i];
+        }
+    std::vector<int> cnt((L + 1) * N, 0);
+    std::vector<double> dsd(torj::kDsNd * N, 0.0);
+    std::vector<int> dsv(torj::kDsNi * N, 0);
+    for (size_t i = 0; i < N; i++) dsv[torj::kDsJ * N + i] = -1;
+    torj::DepoStream dst{dsd.data(), dsv.data()};
+    torj::FitArgs fa{};
+    fa.n = n;
+    fa.n_psi = n_psi;
+    fa.ds = ds;
+    fa.grid = grid;
+    fa.s0 = s0;
+    fa.steps = steps;
+    fa.smp_psi = sp.data();
+    fa.smp_dpds = sd.data();
+    fa.smp_s = nullptr;
+    fa.rows = K;
+    fa.s_uniform = 1;
+    fa.E = E.data(), fa.Gpsi = G1.data(), fa.GP = G2.data();
+    fa.cnt = cnt.data();
+    fa.Fopen = Fo.data();
+    fa.dPs = dp.data();
+    fa.kstar = kstar;
+    fa.Pray = Pray;
+    for (int i = 0; i < n; i++) {
+        for (int S = inc; S < steps[i]; S += inc) torj::fit_depo_stream(fa, dst, i, psiL[i], S);
+        torj::fit_depo_tail(fa, dst, i, psiL[i]);
+    }
+    for (size_t k = 0; k + 1 < L; k++)
+        for (size_t i = 0; i < N; i++) dPs[k * N + i] = dp[k * N + i];
+}
 }

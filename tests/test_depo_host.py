@@ -22,6 +22,7 @@ def H():
     L = C.CDLL(os.path.join(HERE, "native", "build", "libwarm_host.so"))
     L.fd_profile.argtypes = [C.c_int, C.c_int, C.c_int, C.c_double, _dp, _dp, _ip, _dp, _dp, _dp,
                              C.c_int, _dp, _ip, _dp]
+    L.fd_profile_stream.argtypes = L.fd_profile.argtypes
     return L
 
 
@@ -29,7 +30,9 @@ def _d(a):
     return np.ascontiguousarray(a, dtype=np.float64).ctypes.data_as(_dp)
 
 
-def _run(H, n_steps, grid, s0, steps, psiL, smp, nc, ds=1e-4):
+def _run(H, n_steps, grid, s0, steps, psiL, smp, nc, ds=1e-4, stream=0):
+    """nc: the open-shell cache; stream > 0: the streamed walk (fd_profile_stream,
+    the scan's steps growing by `stream` per emulated block)"""
     n = len(s0)
     psi = np.ascontiguousarray(smp[:, :, 0].T)   # (n_steps + 1) x n
     dpds = np.ascontiguousarray(smp[:, :, 1].T)
@@ -37,8 +40,9 @@ def _run(H, n_steps, grid, s0, steps, psiL, smp, nc, ds=1e-4):
     kstar = np.zeros(n, dtype=np.int32)
     P = np.zeros(n)
     st = np.ascontiguousarray(steps, dtype=np.int32)
-    H.fd_profile(n, n_steps, len(grid), ds, _d(grid), _d(s0), st.ctypes.data_as(_ip), _d(psiL),
-                 _d(psi), _d(dpds), nc, _d(dPs), kstar.ctypes.data_as(_ip), _d(P))
+    f = H.fd_profile_stream if stream else H.fd_profile
+    f(n, n_steps, len(grid), ds, _d(grid), _d(s0), st.ctypes.data_as(_ip), _d(psiL),
+      _d(psi), _d(dpds), stream if stream else nc, _d(dPs), kstar.ctypes.data_as(_ip), _d(P))
     return dPs, kstar, P
 
 
@@ -79,6 +83,14 @@ def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode, grid_kind
     for nc in (1, 4):
         d2, k2, P2 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], nc)
         assert np.array_equal(k2, kstar) and np.array_equal(P2, P) and np.array_equal(d2, dPs)
+    # the streamed walk (windows behind the scan, then the tail): independent of
+    # the block schedule bit for bit, and the one-pass walk's result to rounding
+    d60, k60, P60 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], 2, stream=60)
+    d37, k37, P37 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], 2, stream=37)
+    assert np.array_equal(k60, k37) and np.array_equal(P60, P37) and np.array_equal(d60, d37)
+    assert np.array_equal(k60, kstar)
+    assert np.abs(P60 - P).max() <= 1e-13 * P.max()
+    assert np.abs(d60 - dPs).max() <= 1e-13 * np.abs(dPs).max()
 
 
 @pytest.mark.parametrize("periods", [3, 7])
@@ -127,3 +139,11 @@ def test_host_deposition_root_cap_maxn_8(H, oplasma, periods):
     # open-shell spill path under the capped walk
     d1, k1, P1 = _run(H, n_steps, grid, np.array([s0]), np.array([n_steps]), np.array([psiL]), smp, 1, ds)
     assert np.array_equal(d1, dPs) and np.array_equal(k1, kstar) and np.array_equal(P1, P)
+    # the streamed walk detects the runs and redoes the ray whole with the cap
+    d2, k2, P2 = _run(H, n_steps, grid, np.array([s0]), np.array([n_steps]), np.array([psiL]), smp, 2, ds,
+                      stream=60)
+    if periods == 7:
+        assert np.array_equal(d2, dPs) and np.array_equal(k2, kstar) and np.array_equal(P2, P)
+    else:
+        assert np.array_equal(k2, kstar) and abs(P2[0] - P[0]) <= 1e-13 * P[0]
+        assert np.abs(d2 - dPs).max() <= 1e-13 * np.abs(dPs).max()

@@ -107,13 +107,21 @@ struct RayData {
 // bottom up (this sweep stores e_r, g_r with M_r = g_r - e_r M_{r-1}), so the
 // substitution runs upwards in s and fuses with the root walk (walk_ray): one
 // stored sweep instead of two.
-TORJ_HD void nak_eliminate(const RayData &R) {
+TORJ_HD void nak_eliminate_rows(const RayData &R, int r_lo, int r_hi);
+TORJ_HD void nak_eliminate(const RayData &R) { nak_eliminate_rows(R, 1, R.m - 2); }
+
+// Rows r_hi down to r_lo of the same elimination.  r_hi = m - 2 is the whole
+// system's bottom (the not-a-knot end row); a smaller r_hi starts a window of
+// the streamed deposition (k_depo_stream) as if M_{r_hi + 1} were 0: that
+// start's influence on e_r, g_r decays by ~(2 - sqrt 3) = 0.27 per row upwards
+// (1e-23 after the kDepoW rows a window carries past the segments it walks).
+TORJ_HD void nak_eliminate_rows(const RayData &R, int r_lo, int r_hi) {
     const int m = R.m;
-    const double h0 = R.h(0), h1 = R.h(1), hm2 = R.h(m - 2), hm3 = R.h(m - 3);
-    double yn = R.Ypsi(m - 1), yc = R.Ypsi(m - 2), Pn = R.YP(m - 1), Pc = R.YP(m - 2);
-    double hr = R.h(m - 2), ihr = rcp_nz(hr);
+    const double h0 = R.h(0), h1 = R.h(1);
+    double yn = R.Ypsi(r_hi + 1), yc = R.Ypsi(r_hi), Pn = R.YP(r_hi + 1), Pc = R.YP(r_hi);
+    double hr = R.h(r_hi), ihr = rcp_nz(hr);
     double e = 0.0, gp = 0.0, gP = 0.0;
-    for (int r0 = m - 2; r0 >= 1; r0 -= kChunk) {
+    for (int r0 = r_hi; r0 >= r_lo; r0 -= kChunk) {
         double yv[kChunk], Pv[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
@@ -124,7 +132,7 @@ TORJ_HD void nak_eliminate(const RayData &R) {
 #pragma unroll
         for (int u = 0; u < kChunk; u++) {
             const int r = r0 - u;
-            if (r < 1) break;
+            if (r < r_lo) break;
             const double hl = R.h(r - 1), ihl = rcp_nz(hl);
             const double yl = yv[u], Pl = Pv[u];
             const double rp = 6.0 * ((yn - yc) * ihr - (yc - yl) * ihl);
@@ -136,6 +144,7 @@ TORJ_HD void nak_eliminate(const RayData &R) {
                 sub = 0.0;
             }
             if (r == m - 2) {
+                const double hm2 = hr, hm3 = hl;  // h(m - 2), h(m - 3)
                 sub = hm3 - hm2 * hm2 / hm3;
                 dia = 2.0 * hm3 + 3.0 * hm2 + hm2 * hm2 / hm3;
                 sup = 0.0;
@@ -405,21 +414,37 @@ TORJ_HD void walk_segment(W_ &W, const Cubic &qs, double y1, const Cubic &qP, bo
     W.Fhi = sum;
 }
 
-// the root walk over the segments, with the spline's second derivatives from
-// the upward substitution M_r = g_r - e_r M_{r-1} (nak_eliminate) as it goes
+// The walk's position: segment j is next, with (M_j, M_{j+1}, M_{j+2}) of the psi
+// and dP/ds splines and the data at point j (psi, dP/ds).
+struct WalkCarry {
+    double Ml, Mr, Mn, MPl, MPr, MPn, yl, Pl;
+    int j;
+};
+
+// the walk's start (segment 0): rows 1 and 2 of the elimination are final
 template <class W_>
-TORJ_HD void walk_ray(W_ &W, const RayData &R) {
-    const int m = R.m;
-    const double q0 = R.h(0) / R.h(1), q1 = R.h(m - 2) / R.h(m - 3);
+TORJ_HD void walk_start(W_ &W, const RayData &R, WalkCarry &C) {
+    const double q0 = R.h(0) / R.h(1);
     const double M1 = R.GPSI(1), M1P = R.GPP(1);
     const double M2 = R.GPSI(2) - R.EE(2) * M1, M2P = R.GPP(2) - R.EE(2) * M1P;
-    // segment j uses (M_j, M_{j+1}); M_{j+2} is prepared for the next one
-    double Ml = (1.0 + q0) * M1 - q0 * M2, MPl = (1.0 + q0) * M1P - q0 * M2P;
-    double Mr = M1, MPr = M1P, Mn = M2, MPn = M2P;
-    double yl = R.Ypsi(0), Pl = R.YP(0);
-    W.cur.c = level_above(*W.a, yl, true);  // #boundaries <= psi(s = 0)
+    C.Ml = (1.0 + q0) * M1 - q0 * M2, C.MPl = (1.0 + q0) * M1P - q0 * M2P;
+    C.Mr = M1, C.MPr = M1P, C.Mn = M2, C.MPn = M2P;
+    C.yl = R.Ypsi(0), C.Pl = R.YP(0);
+    C.j = 0;
+    W.cur.c = level_above(*W.a, C.yl, true);  // #boundaries <= psi(s = 0)
     W.cur.load();
-    for (int j0 = 0; j0 + 1 < m; j0 += kWalkChunk) {
+}
+
+// the root walk over segments [C.j, j_end), with the spline's second
+// derivatives from the upward substitution M_r = g_r - e_r M_{r-1}
+// (nak_eliminate) as it goes; rows C.j + 3 .. j_end + 2 (at most m - 2) of the
+// elimination are final
+template <class W_>
+TORJ_HD void walk_segments(W_ &W, const RayData &R, WalkCarry &C, int j_end) {
+    const int m = R.m;
+    double Ml = C.Ml, Mr = C.Mr, Mn = C.Mn, MPl = C.MPl, MPr = C.MPr, MPn = C.MPn;
+    double yl = C.yl, Pl = C.Pl;
+    for (int j0 = C.j; j0 < j_end; j0 += kWalkChunk) {
         double yv[kWalkChunk], Pv[kWalkChunk], ev[kWalkChunk], gv[kWalkChunk], gPv[kWalkChunk];
 #pragma unroll
         for (int u = 0; u < kWalkChunk; u++) {
@@ -434,7 +459,7 @@ TORJ_HD void walk_ray(W_ &W, const RayData &R) {
 #pragma unroll
         for (int u = 0; u < kWalkChunk; u++) {
             const int j = j0 + u;
-            if (j + 1 >= m) break;
+            if (j >= j_end) break;
             const double h = R.h(j), ih = rcp_nz(h);
             const Cubic qs = make_cubic(yl, yv[u], Ml, Mr, h, ih), qP = make_cubic(Pl, Pv[u], MPl, MPr, h, ih);
             walk_segment(W, qs, yv[u], qP, j == 0);
@@ -445,31 +470,29 @@ TORJ_HD void walk_ray(W_ &W, const RayData &R) {
                 Mn = gv[u] - ev[u] * Mr;
                 MPn = gPv[u] - ev[u] * MPr;
             } else if (j + 3 == m - 1) {  // not-a-knot end: M_{m-1} from M_{m-2}, M_{m-3}
+                const double q1 = R.h(m - 2) / R.h(m - 3);
                 Mn = (1.0 + q1) * Mr - q1 * Ml;
                 MPn = (1.0 + q1) * MPr - q1 * MPl;
             }
         }
     }
+    C.Ml = Ml, C.Mr = Mr, C.Mn = Mn, C.MPl = MPl, C.MPr = MPr, C.MPn = MPn;
+    C.yl = yl, C.Pl = Pl;
+    C.j = j_end;
 }
 
+template <class W_>
+TORJ_HD void walk_ray(W_ &W, const RayData &R) {
+    WalkCarry C;
+    walk_start(W, R, C);
+    walk_segments(W, R, C, R.m - 1);
+}
 
-// One ray of power_deposition_profile (k_fit_depo; the CPU suite runs the host
-// build through tests/native): spline fits, the root walk, the outside-in break
-// shell k* and the ray's deposited power P.  psiL = psi at the launch point.
+// The walk's end: flush the last root run, redo a ray whose psi(s) has more
+// than kMaxRoots monotone runs with the root cap, then the reference's
+// outside-in break shell k* and the ray's deposited power P.
 template <int NC>
-TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
-    // a trace: launch point, entry point, one per step; or the caller's points
-    const int m = a.npts ? a.npts[i] : a.steps[i] + 2;
-    if (m < 4 || (!a.npts && !(a.s0[i] > 0.0))) {  // FITPACK needs > k = 3 strictly increasing points
-        a.kstar[i] = a.n_psi;  // no shell counts
-        a.Pray[i] = 0.0;
-        return;
-    }
-    RayData R{&a, i, m, a.npts ? 0.0 : a.s0[i], psiL};
-    nak_eliminate(R);
-    Walker<NC> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
-    W.init();
-    walk_ray(W, R);
+TORJ_HD void fit_depo_finish(const FitArgs &a, int i, const RayData &R, Walker<NC> &W) {
     W.flush_run();
     // the walk's root counts and shell sums are no-return atomics: wait for them
     // before this lane reads its own counts back
@@ -490,6 +513,9 @@ TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #endif
+        // the whole-ray elimination again (a streamed walk's windows left other
+        // rows behind; for fit_depo_ray the same values)
+        nak_eliminate(R);
         Walker<NC, true> Wc{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
         Wc.init();
         walk_ray(Wc, R);
@@ -532,6 +558,137 @@ TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
             if (q0 - u > kstar) P += v[u];
     }
     a.Pray[i] = P;
+}
+
+// One ray of power_deposition_profile (k_fit_depo; the CPU suite runs the host
+// build through tests/native): spline fits, the root walk, the outside-in break
+// shell k* and the ray's deposited power P.  psiL = psi at the launch point.
+template <int NC>
+TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
+    // a trace: launch point, entry point, one per step; or the caller's points
+    const int m = a.npts ? a.npts[i] : a.steps[i] + 2;
+    if (m < 4 || (!a.npts && !(a.s0[i] > 0.0))) {  // FITPACK needs > k = 3 strictly increasing points
+        a.kstar[i] = a.n_psi;  // no shell counts
+        a.Pray[i] = 0.0;
+        return;
+    }
+    RayData R{&a, i, m, a.npts ? 0.0 : a.s0[i], psiL};
+    nak_eliminate(R);
+    Walker<NC> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
+    walk_ray(W, R);
+    fit_depo_finish(a, i, R, W);
+}
+
+// ---------------------------------------------------------------------------
+// Streamed deposition (the split pipeline): the walk advances in windows of
+// kDepoQ segments while the trace is still running, one k_depo_stream launch
+// after each block's optical-depth scan, and k_depo_tail finishes every ray
+// after the trace.  A window [j, j + kDepoQ) eliminates rows j + 3 ..
+// j + kDepoQ + 2 + kDepoW from a start kDepoW rows below the last row it uses
+// (nak_eliminate_rows), so it needs the ray's points up to j + kDepoQ + 3 +
+// kDepoW and never the not-a-knot end.  Window boundaries are multiples of
+// kDepoQ whatever the launch schedule (block size, ray batch) and each window
+// recomputes its own rows, so the results do not depend on when the windows
+// ran.  The rest of the ray after the last window that fits below its end
+// point m - 2 is the exact elimination of the unstreamed kernel; a ray with no
+// window (m < kDepoQ + kDepoW + 5) is exactly fit_depo_ray.  Against the one
+// global elimination the second derivatives move by rounding only (the window
+// start's influence is ~1e-23 where it is used).
+constexpr int kDepoQ = 64, kDepoW = 40;
+// one ray's walk between launches, SoA [field][n]
+enum { kDsFhi, kDsFlo, kDsOF0, kDsOF1, kDsMl, kDsMr, kDsMn, kDsMPl, kDsMPr, kDsMPn, kDsYl, kDsPl, kDsNd };
+enum { kDsJ, kDsC, kDsOQ0, kDsOQ1, kDsSpill, kDsRk0, kDsRk1, kDsRd, kDsRuns, kDsLast, kDsNi };
+struct DepoStream {
+    double *d;  // kDsNd x n
+    int *v;     // kDsNi x n; v[kDsJ] = -1: not started
+};
+static_assert(kOpenCache == 2, "DepoStream holds two open-shell slots");
+
+// the walk's state of ray i from / to the stream arrays; false: not started
+TORJ_HD bool depo_load(const DepoStream &ds, size_t n, int i, Walker<kOpenCache> &W, WalkCarry &C) {
+    const int j = ds.v[kDsJ * n + i];
+    if (j < 0) return false;
+    const double *d = ds.d + i;
+    const int *v = ds.v + i;
+    W.Fhi = d[kDsFhi * n], W.Flo = d[kDsFlo * n];
+    W.oF[0] = d[kDsOF0 * n], W.oF[1] = d[kDsOF1 * n];
+    C.Ml = d[kDsMl * n], C.Mr = d[kDsMr * n], C.Mn = d[kDsMn * n];
+    C.MPl = d[kDsMPl * n], C.MPr = d[kDsMPr * n], C.MPn = d[kDsMPn * n];
+    C.yl = d[kDsYl * n], C.Pl = d[kDsPl * n];
+    C.j = j;
+    W.cur.c = v[kDsC * n];
+    W.cur.load();
+    W.oq[0] = v[kDsOQ0 * n], W.oq[1] = v[kDsOQ1 * n];
+    W.spilled = v[kDsSpill * n] != 0;
+    W.run_k0 = v[kDsRk0 * n], W.run_k1 = v[kDsRk1 * n], W.run_d = v[kDsRd * n];
+    W.runs = v[kDsRuns * n], W.last_d = v[kDsLast * n];
+    return true;
+}
+TORJ_HD void depo_save(const DepoStream &ds, size_t n, int i, const Walker<kOpenCache> &W, const WalkCarry &C) {
+    double *d = ds.d + i;
+    int *v = ds.v + i;
+    d[kDsFhi * n] = W.Fhi, d[kDsFlo * n] = W.Flo;
+    d[kDsOF0 * n] = W.oF[0], d[kDsOF1 * n] = W.oF[1];
+    d[kDsMl * n] = C.Ml, d[kDsMr * n] = C.Mr, d[kDsMn * n] = C.Mn;
+    d[kDsMPl * n] = C.MPl, d[kDsMPr * n] = C.MPr, d[kDsMPn * n] = C.MPn;
+    d[kDsYl * n] = C.yl, d[kDsPl * n] = C.Pl;
+    v[kDsC * n] = W.cur.c;
+    v[kDsOQ0 * n] = W.oq[0], v[kDsOQ1 * n] = W.oq[1];
+    v[kDsSpill * n] = W.spilled ? 1 : 0;
+    v[kDsRk0 * n] = W.run_k0, v[kDsRk1 * n] = W.run_k1, v[kDsRd * n] = W.run_d;
+    v[kDsRuns * n] = W.runs, v[kDsLast * n] = W.last_d;
+    v[kDsJ * n] = C.j;
+}
+
+// every whole window whose rows lie at or above row `last` (points up to
+// `last` available, last <= m - 2); returns whether the walk has started
+TORJ_HD bool depo_windows(const RayData &R, Walker<kOpenCache> &W, WalkCarry &C, bool started, int last) {
+    for (;;) {
+        const int ja = started ? C.j : 0, jb = ja + kDepoQ, r0 = jb + 2 + kDepoW;
+        if (r0 + 1 > last) break;
+        nak_eliminate_rows(R, started ? ja + 3 : 1, r0);
+        if (!started) {
+            walk_start(W, R, C);
+            started = true;
+        }
+        walk_segments(W, R, C, jb);
+    }
+    return started;
+}
+
+// k_depo_stream: ray i's windows over its first S steps (the scan has passed
+// them and the ray is still running, so its end point lies beyond them)
+TORJ_HD void fit_depo_stream(const FitArgs &a, const DepoStream &ds, int i, double psiL, int S) {
+    if (!(a.s0[i] > 0.0)) return;
+    const int j = ds.v[kDsJ * (size_t)a.n + i];
+    if ((j < 0 ? 0 : j) + kDepoQ + 3 + kDepoW > S) return;  // no new window yet
+    RayData R{&a, i, S + 2, a.s0[i], psiL};
+    Walker<kOpenCache> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
+    WalkCarry C{};
+    const bool started = depo_load(ds, a.n, i, W, C);
+    if (depo_windows(R, W, C, started, S)) depo_save(ds, a.n, i, W, C);
+}
+
+// k_depo_tail: the windows still left, the exact rest of the ray, the finish
+TORJ_HD void fit_depo_tail(const FitArgs &a, const DepoStream &ds, int i, double psiL) {
+    const int m = a.steps[i] + 2;
+    if (m < 4 || !(a.s0[i] > 0.0)) {  // as fit_depo_ray (no window ever ran for such a ray)
+        a.kstar[i] = a.n_psi;
+        a.Pray[i] = 0.0;
+        return;
+    }
+    RayData R{&a, i, m, a.s0[i], psiL};
+    Walker<kOpenCache> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
+    WalkCarry C{};
+    bool started = depo_load(ds, a.n, i, W, C);
+    started = depo_windows(R, W, C, started, m - 2);
+    nak_eliminate_rows(R, started ? C.j + 3 : 1, m - 2);
+    if (!started) walk_start(W, R, C);
+    walk_segments(W, R, C, m - 1);
+    fit_depo_finish(a, i, R, W);
 }
 
 }  // namespace torj

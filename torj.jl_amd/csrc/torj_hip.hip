@@ -1409,6 +1409,33 @@ __global__ void __launch_bounds__(64, 2) k_fit_depo(FitArgs a) {
     const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
     fit_depo_ray<kOpenCache>(a, i, psi_at(a.coef, a.g, xl));
 }
+// the streamed deposition (torj_fitdepo.hpp): windows of the walk behind the
+// split pipeline's scan (S = the scan's steps of a still-running ray), then the
+// rest of every ray after the trace
+__device__ __forceinline__ bool fit_grid_lds(FitArgs &a) {
+    extern __shared__ double s_grid[];
+    if (a.n_psi > kFitGridLds) return false;
+    for (int k = threadIdx.x; k < a.n_psi; k += 64) s_grid[k] = a.grid[k];
+    __syncthreads();
+    a.grid = s_grid;
+    return true;
+}
+__global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds, const int *sinfo) {
+    fit_grid_lds(a);
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const int v = sinfo[i];
+    if (info_status(v) != ST_OK) return;  // stopped: k_depo_tail takes the rest
+    const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
+    fit_depo_stream(a, ds, i, psi_at(a.coef, a.g, xl), info_steps(v));
+}
+__global__ void __launch_bounds__(64, 2) k_depo_tail(FitArgs a, DepoStream ds) {
+    fit_grid_lds(a);
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= a.n) return;
+    const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
+    fit_depo_tail(a, ds, i, psi_at(a.coef, a.g, xl));
+}
 // torj_power_deposition_profile: the caller's vectors of ray i (points off[i] ..
 // off[i] + npts[i] - 1) into the fit's per-point rows, psi(s_j) from the psi
 // spline at x_j (src/plasma.jl:95-98: psi_norm_spline(hypot(x, y), z))
@@ -2410,7 +2437,8 @@ int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N
 // kernels on its low-priority one, a ring of kRing alpha-input buffers so the
 // trajectory runs up to kRing blocks ahead of the alpha; forked from and
 // joined back into `s`.
-static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, hipStream_t s) {
+static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, hipStream_t s,
+                       const FitArgs *fa, DepoStream *dso) {
     const size_t n = (size_t)a.n;
     const int n_steps = a.n_steps;
     // steps per block: kRing alpha-input buffers within the budget (TORJ_SPLIT_MB
@@ -2441,8 +2469,17 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
     const int nq = (int)((n + 255) / 256);
+    // the streamed deposition's per-ray walk state (fa: the reference profile;
+    // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
+    static const int dstream_env = [] {
+        const char *e = getenv("TORJ_DEPO_STREAM");
+        return e ? atoi(e) : 1;
+    }();
+    const bool dstream = fa && dso && dstream_env != 0;
+    const size_t b_dsd = dstream ? al(kDsNd * sizeof(double) * n) : 0,
+                 b_dsi = dstream ? al(kDsNi * sizeof(int) * n) : 0;
     const size_t bytes = R * (b_ain + b_alpha + b_awork) + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
-                         2 * b_n4;
+                         2 * b_n4 + b_dsd + b_dsi;
     if (ensure_split(p, bytes)) return -1;
     char *q = (char *)p->d_split;
     auto take = [&](size_t b) {
@@ -2470,6 +2507,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     sp.sPdep = (double *)take(b_n8);
     sp.tinfo = (int *)take(b_n4);
     sp.sinfo = (int *)take(b_n4);
+    DepoStream ds{};
+    if (dstream) {
+        ds.d = (double *)take(b_dsd);
+        ds.v = (int *)take(b_dsi);
+        *dso = ds;
+    } else if (dso) {
+        *dso = DepoStream{};
+    }
 
     // TORJ_SPLIT_SERIAL=1: every kernel on the caller's stream, no overlap (a
     // measurement aid; read per call so a test can compare both orders)
@@ -2493,6 +2538,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // the scan's carry starts at (steps 0, OK), tau = 0, P_dep = 0
     HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, sT));
     HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, sT));
+    if (dstream) HIPCK(hipMemsetAsync(ds.v + kDsJ * n, 0xFF, n * sizeof(int), sT));  // j = -1: not started
+    const size_t fit_lds = fa && fa->n_psi <= kFitGridLds ? (size_t)fa->n_psi * sizeof(double) : 0;
     const int G = (int)((n + 63) / 64);
     // the trajectory kernel with the coefficients staged in LDS whenever the grid
     // fits 160 KiB at 6 fp64 per node (56 x 56: 161 KB), one workgroup of wpb
@@ -2551,6 +2598,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         else
             TORJ_SPLIT_DISPATCH(k_tau_scan, dim3(G), dim3(64), 0, s3, a, sp);
         HIPCK(hipEventRecord(p->ev_S[r], s3));
+        // the deposition walk's windows behind this scan (same stream: after it,
+        // and the next scan after them; the ring slot is already released)
+        if (dstream && b + 1 < n_blocks) hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, s3, *fa, ds, sp.sinfo);
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
 #undef TORJ_SPLIT_DISPATCH
@@ -2792,6 +2842,7 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     if (depo)  // psi_dP_dV strictly increasing: checked on the device, reported by torj_trace_check
         hipLaunchKernelGGL(k_grid_check, dim3(1), dim3(256), 0, s, grid, n_psi, p->d_flags);
     const int DM = !depo ? kDepoNone : (fit ? kDepoSamples : kDepoBinned);
+    DepoStream dstr{};  // the split pipeline's streamed deposition (split_trace)
     if (tr) {
         a.traj_stride = cfg->traj_stride;
         a.n_save = cfg->n_steps / cfg->traj_stride;
@@ -2889,7 +2940,7 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
                            cfg->n_steps < kSplitMaxSteps &&
                            (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
     if (use_split) {
-        if (split_trace(p, a, DM, tr, cs, s)) return -1;
+        if (split_trace(p, a, DM, tr, cs, s, fit ? &fa : nullptr, &dstr)) return -1;
     } else if (use_sched && cfg->n_steps > 0) {
         // W persistent waves: at most 2 per SIMD (4 SIMDs per CU), and fewer
         // than G so the ready queue keeps a backlog (a wave never waits for a
@@ -2974,7 +3025,10 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
         else
             hipLaunchKernelGGL(k_final_alpha<0>, dim3(nblocks(n, 64)), dim3(64), 0, s, a);
         const size_t lds = n_psi <= kFitGridLds ? (size_t)n_psi * sizeof(double) : 0;
-        hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), lds, s, fa);
+        if (dstr.v)  // the streamed walk's windows ran behind the scans
+            hipLaunchKernelGGL(k_depo_tail, dim3(nblocks(n, 64)), dim3(64), lds, s, fa, dstr);
+        else
+            hipLaunchKernelGGL(k_fit_depo, dim3(nblocks(n, 64)), dim3(64), lds, s, fa);
         hipLaunchKernelGGL(k_shell_sum, dim3(n_psi), dim3(256), 0, s, fa);
         HIPCK(hipGetLastError());
     }
