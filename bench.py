@@ -318,8 +318,11 @@ def main():
                                   if traffic and traffic.get("fp64_flops_executed") else None),
                 "kernel": kname,
                 "kernel_ms": kern_s * 1e3,
-                "kernel_ms_note": ("the trace phase: the split pipeline's kernels overlapped on two "
-                                   "streams, HIP events on the launch stream around all of them"
+                "kernel_ms_note": ("the trace phase: the split pipeline's kernels (trajectory, alpha, "
+                                   "tau scan and, for the reference profile, the deposition walk's "
+                                   "streamed windows, whose work the FLOP count does not price) "
+                                   "overlapped on three streams, HIP events on the launch stream "
+                                   "around all of them"
                                    if split else "HIP events around the trace kernel"),
                 "rocprof_per_launch_ms": traffic.get("rocprof_per_launch_ms") if traffic else None,
                 "deposition_kernels_ms": float(km[1].item()),

@@ -11,10 +11,10 @@ timeout -k 10 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeou
 tail -2 $O/pytest_gpu.log
 timeout -k 10 300 python scripts/alpha_sweep_stats.py > $O/profiles/alpha_sweep.json 2> $O/alpha_sweep.err || { tail -20 $O/alpha_sweep.err; exit 1; }
 bash scripts/profile.sh prof_c3 || exit 1
-python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles "k_traj|k_alpha_pts|k_tau_scan|k_split_final" || exit 1
-python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_fit_depo depo_ || exit 1
+python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles "k_traj|k_alpha_pts|k_tau_scan|k_split_final|k_depo_stream" || exit 1
+python tools/prof_summary.py gpurun_out/prof_c3 $O/profiles k_depo_tail depo_ || exit 1
 bash scripts/profile.sh prof_c5 --absorption warm_wr || exit 1
-python tools/prof_summary.py gpurun_out/prof_c5 $O/profiles "k_traj|k_alpha_warm_pts|k_tau_scan|k_split_final" c5_ || exit 1
+python tools/prof_summary.py gpurun_out/prof_c5 $O/profiles "k_traj|k_alpha_warm_pts|k_tau_scan|k_split_final|k_depo_stream" c5_ || exit 1
 mkdir -p profiles/$R && cp $O/profiles/*.json $O/profiles/*.csv profiles/$R/ 2>/dev/null
 timeout -k 10 600 python bench.py > $O/bench_c3.log 2>&1 || { tail -20 $O/bench_c3.log; exit 1; }
 grep '^{' $O/bench_c3.log

@@ -114,7 +114,7 @@ TORJ_HD void nak_eliminate(const RayData &R) { nak_eliminate_rows(R, 1, R.m - 2)
 // system's bottom (the not-a-knot end row); a smaller r_hi starts a window of
 // the streamed deposition (k_depo_stream) as if M_{r_hi + 1} were 0: that
 // start's influence on e_r, g_r decays by ~(2 - sqrt 3) = 0.27 per row upwards
-// (1e-23 after the kDepoW rows a window carries past the segments it walks).
+// (5e-19 after the kDepoW rows a window carries past the segments it walks).
 TORJ_HD void nak_eliminate_rows(const RayData &R, int r_lo, int r_hi) {
     const int m = R.m;
     const double h0 = R.h(0), h1 = R.h(1);
@@ -594,8 +594,8 @@ TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
 // point m - 2 is the exact elimination of the unstreamed kernel; a ray with no
 // window (m < kDepoQ + kDepoW + 5) is exactly fit_depo_ray.  Against the one
 // global elimination the second derivatives move by rounding only (the window
-// start's influence is ~1e-23 where it is used).
-constexpr int kDepoQ = 64, kDepoW = 40;
+// start's influence is ~5e-19 where it is used).
+constexpr int kDepoQ = 64, kDepoW = 32;
 // one ray's walk between launches, SoA [field][n]
 enum { kDsFhi, kDsFlo, kDsOF0, kDsOF1, kDsMl, kDsMr, kDsMn, kDsMPl, kDsMPr, kDsMPn, kDsYl, kDsPl, kDsNd };
 enum { kDsJ, kDsC, kDsOQ0, kDsOQ1, kDsSpill, kDsRk0, kDsRk1, kDsRd, kDsRuns, kDsLast, kDsNi };

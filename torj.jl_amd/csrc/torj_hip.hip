@@ -2600,6 +2600,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         HIPCK(hipEventRecord(p->ev_S[r], s3));
         // the deposition walk's windows behind this scan (same stream: after it,
         // and the next scan after them; the ring slot is already released)
+        // (measured on the headline beam: after every block on the scan's stream
+        // 3.62-3.63e9 ray-steps/s; every 2nd / 4th block 3.45-3.64 / 3.58-3.59e9;
+        // behind the alpha or the trajectory kernel's stream 3.03 / 2.98e9)
         if (dstream && b + 1 < n_blocks) hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, s3, *fa, ds, sp.sinfo);
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
