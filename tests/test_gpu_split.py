@@ -290,3 +290,36 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
         assert c0[7] == 0 and c1[7] > 0 and c1[2] < c0[2] and c1[5] < c0[5], (c0, c1)
         assert c1[5] + c1[7] >= c0[5], (c0, c1)
     assert np.array_equal(cnts["1", 3], cnts["1", 0])
+
+
+def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
+    """The reference profile's root walk streamed in windows behind each block's
+    scan (k_depo_stream + k_depo_tail, torj_fitdepo.hpp) against the one-pass
+    k_fit_depo after the trace (TORJ_DEPO_STREAM=0): the trace itself is
+    bit-identical, the deposited power per ray and per shell equal to rounding
+    (<= 1e-13), with rays ABSORBED mid-trace (the tail takes stopped rays) and
+    blocks of 90 steps that do not align with the 64-segment windows."""
+    import os
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=3000, chunk_steps=30, weights=w, traj_stride=30, P_min=5e-2,
+              psi_grid=np.linspace(0, 1, 500), deposition="reference", x_launch=pos, s0=s0)
+    out = {}
+    old = os.environ.get("TORJ_DEPO_STREAM")
+    try:
+        for mode in ("0", "1"):
+            os.environ["TORJ_DEPO_STREAM"] = mode
+            out[mode] = _run(T, hplasma, 3, 90, xp, Np, om, 1, **kw)
+    finally:
+        if old is None:
+            os.environ.pop("TORJ_DEPO_STREAM", None)
+        else:
+            os.environ["TORJ_DEPO_STREAM"] = old
+    a, b = out["0"], out["1"]
+    st = a.status.tolist()
+    assert st.count(T.ABSORBED) >= 10 and a.steps.max() > 1000, "need long rays and mid-trace stops"
+    for f in ("state", "status", "steps"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.abs(a.P_dep - b.P_dep).max() <= 1e-13 * np.abs(a.P_dep).max()
+    assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
+    assert np.abs(a.dP_shell).max() > 0

@@ -2471,10 +2471,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int nq = (int)((n + 255) / 256);
     // the streamed deposition's per-ray walk state (fa: the reference profile;
     // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
-    static const int dstream_env = [] {
-        const char *e = getenv("TORJ_DEPO_STREAM");
-        return e ? atoi(e) : 1;
-    }();
+    const char *dstream_e = getenv("TORJ_DEPO_STREAM");  // read per call (tests compare both)
+    const int dstream_env = dstream_e ? atoi(dstream_e) : 1;
     const bool dstream = fa && dso && dstream_env != 0;
     const size_t b_dsd = dstream ? al(kDsNd * sizeof(double) * n) : 0,
                  b_dsi = dstream ? al(kDsNi * sizeof(int) * n) : 0;
