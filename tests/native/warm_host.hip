@@ -167,7 +167,9 @@ void fd_profile_stream(int n, int n_steps, int n_psi, double ds, const double *g
     fa.kstar = kstar;
     fa.Pray = Pray;
     for (int i = 0; i < n; i++) {
-        for (int S = inc; S < steps[i]; S += inc) torj::fit_depo_stream(fa, dst, i, psiL[i], S);
+        // as k_depo_stream: psi at the launch point only for the walk's start
+        for (int S = inc; S < steps[i]; S += inc)
+            torj::fit_depo_stream(fa, dst, i, dsv[torj::kDsJ * N + i] < 0 ? psiL[i] : 0.0, S);
         torj::fit_depo_tail(fa, dst, i, psiL[i]);
     }
     for (size_t k = 0; k + 1 < L; k++)

@@ -1426,8 +1426,15 @@ __global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds,
     if (i >= a.n) return;
     const int v = sinfo[i];
     if (info_status(v) != ST_OK) return;  // stopped: k_depo_tail takes the rest
-    const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
-    fit_depo_stream(a, ds, i, psi_at(a.coef, a.g, xl), info_steps(v));
+    const int S = info_steps(v), j = ds.v[kDsJ * (size_t)a.n + i];
+    if ((j < 0 ? 0 : j) + kDepoQ + 3 + kDepoW > S) return;  // no new window yet
+    // psi at the launch point (point 0) enters only the walk's start
+    double psiL = 0.0;
+    if (j < 0) {
+        const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
+        psiL = psi_at(a.coef, a.g, xl);
+    }
+    fit_depo_stream(a, ds, i, psiL, S);
 }
 __global__ void __launch_bounds__(64, 2) k_depo_tail(FitArgs a, DepoStream ds) {
     fit_grid_lds(a);
