@@ -224,7 +224,7 @@ class OraclePlasma:
                           1.0 / self.grad_norm(x, N, omega, mode), mode,
                           1 if model == 2 else 3)[0]
 
-    def warm_sensitivity(self, x0, N0, omega, mode, ds, steps, iwarm=1, eta=2.0 ** -46,
+    def warm_sensitivity(self, x0, N0, omega, mode, ds, steps, iwarm=1, eta=2.0 ** -45,
                          n_threads=None):
         """or_warm_sensitivity: per ray, sum over its RK4 stage points (first
         steps[r] steps) of ds w_stage max |d alpha| under relative input

@@ -4,7 +4,7 @@
 # gpurun_out/round/ (profiles copied to profiles/$ROUND/ in the tree that travels
 # back under gpurun_out/round/profiles)
 cd "$GRAFT_REPO_ROOT" || exit 1
-R=${ROUND:-r03}
+R=${ROUND:-r04}
 O=gpurun_out/round
 mkdir -p $O/profiles
 timeout -k 10 1200 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }

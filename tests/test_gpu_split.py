@@ -295,7 +295,8 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
 def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     """The reference profile's root walk streamed in windows behind each block's
     scan (k_depo_stream + k_depo_tail, torj_fitdepo.hpp) against the one-pass
-    k_fit_depo after the trace (TORJ_DEPO_STREAM=0): the trace itself is
+    k_fit_depo after the trace (TORJ_DEPO_STREAM=0), and the windows on a stream
+    of their own (=2) against the scan's stream (=1): the trace itself is
     bit-identical, the deposited power per ray and per shell equal to rounding
     (<= 1e-13), with rays ABSORBED mid-trace (the tail takes stopped rays) and
     blocks of 90 steps that do not align with the 64-segment windows."""
@@ -307,7 +308,7 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     out = {}
     old = os.environ.get("TORJ_DEPO_STREAM")
     try:
-        for mode in ("0", "1"):
+        for mode in ("0", "1", "2"):
             os.environ["TORJ_DEPO_STREAM"] = mode
             out[mode] = _run(T, hplasma, 3, 90, xp, Np, om, 1, **kw)
     finally:
@@ -323,3 +324,65 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     assert np.abs(a.P_dep - b.P_dep).max() <= 1e-13 * np.abs(a.P_dep).max()
     assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-13 * np.abs(a.dP_shell).max()
     assert np.abs(a.dP_shell).max() > 0
+    # the windows on a stream of their own (TORJ_DEPO_STREAM=2, overlapping the
+    # next block's scan): the same windows, so the same bits as on the scan's stream
+    c = out["2"]
+    for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+        assert np.array_equal(getattr(b, f), getattr(c, f)), f
+
+
+def _env_run(T, hplasma, env, *args, **kw):
+    import os
+
+    old = {k: os.environ.get(k) for k in env}
+    try:
+        for k, v in env.items():
+            os.environ[k] = v
+        return _run(T, hplasma, 3, 60, *args, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_traj_tile_bit_identical_to_global_fallback(gpu, T, hplasma):
+    """k_traj_tile (TORJ_TRAJ_LDS=2) stages per wave only the coefficient tile
+    its rays can reach in the block and reads a stencil outside it from global
+    memory (torj_hip.hip traj_body).  The same kernel with the tile's margin at
+    0 (rays leave their tile mid-block: the per-evaluation fallback), with a
+    30-node cap (some waves untiled) and with no tile at all gives bit-identical
+    outputs; against the whole-grid LDS kernel and the L2 kernel (separately
+    compiled) to 1e-12, statuses and steps exact."""
+    from test_gpu_c3 import _close
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, psi_grid=np.linspace(0, 1, 1000),
+              deposition="reference", x_launch=pos, s0=s0)
+    ref = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": "2"}, xp, Np, om, 1, **kw)
+    for env in ({"TORJ_TILE_MARGIN": "0"}, {"TORJ_TILE_CAP": "30"}, {"TORJ_TILE_CAP": "0"}):
+        r = _env_run(T, hplasma, dict(env, TORJ_TRAJ_LDS="2"), xp, Np, om, 1, **kw)
+        for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+            assert np.array_equal(getattr(ref, f), getattr(r, f)), (env, f)
+        assert np.array_equal(ref.traj, r.traj, equal_nan=True), env
+    for mode in ("1", "0"):
+        r = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, **kw)
+        _close(ref, r, 1e-12)
+        print(f"TORJ_TRAJ_LDS={mode} vs tile: bit-identical state "
+              f"{np.array_equal(ref.state, r.state)}")
+
+
+def test_traj_tile_vs_oracle_with_stops(gpu, T, hplasma, oplasma):
+    """The tiled trajectory kernel against the oracle with ABSORBED and
+    LEFT_PLASMA stops mid-block (as test_split_termination_vs_oracle)."""
+    from test_gpu_parity import _compare_trace
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma, n_rings=4)
+    grid = np.linspace(0, 1, 300)
+    kw = dict(ds=1e-4, n_steps=4000, chunk_steps=40, psi_grid=grid, traj_stride=50, P_min=1e-2)
+    g = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": "2", "TORJ_TILE_MARGIN": "0.5"}, xp, Np, om, 1, **kw)
+    o = oplasma.trace(xp, Np, om, 1, 1e-4, 4000, chunk_steps=40, psi_grid=grid, traj_stride=50,
+                      P_min=1e-2)
+    _compare_trace(g, o)
+    assert np.abs(g.dP_shell[:-1] - o["dP"]).max() <= 1e-10 * np.abs(o["dP"]).max()

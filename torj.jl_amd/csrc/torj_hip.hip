@@ -897,6 +897,8 @@ struct SplitArgs {
     int *sinfo;           // steps | status << 24: the scan's stop
     int k0, kb;           // block: steps [k0, k0 + kb)
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
+    int tile_cap;         // k_traj_tile: most nodes a wave stages (<= kTileNodes)
+    double tile_margin;   // k_traj_tile: the box's margin in units of the block's path, (kb + 1) ds
 };
 
 // steps | status << 24: split launches need n_steps < kSplitMaxSteps (the
@@ -908,8 +910,8 @@ __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st
 
 // One cold RK4 step of ray_segment's arithmetic (plasma_point with ln Te, as
 // the absorbing kernels evaluate it); STORE: this step's alpha inputs -> ain.
-template <bool STORE, int NS = kNF>
-__device__ __forceinline__ bool cold_step(const TraceArgs &a, const double *__restrict__ coef,
+template <bool STORE, int NS = kNF, class CS = const double *>
+__device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
                                           const SplitArgs &sp, int j, int i, const double x[3],
                                           const double N[3], double xn[3], double Nn[3]) {
     const double hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
@@ -969,35 +971,45 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, const double *__re
 #ifndef TORJ_ALPHA_UNROLL  // node pairs per iteration of the alpha kernel's node loop (ILP)
 #define TORJ_ALPHA_UNROLL 1
 #endif
-// LDS: the field coefficients staged in LDS (6 fp64 per node, 161 KB for a 56 x 56
-// grid; one workgroup of up to 8 waves per CU), measured against L2
+// Where the trajectory kernel reads the field coefficients:
+//   kTrajL2    the global array through L1 / L2 (any grid);
+//   kTrajLds   the whole grid staged in LDS (6 fp64 per node, 161 KB for a 56 x 56
+//              grid: one workgroup of up to 8 waves per CU);
+//   kTrajTile  per wave and block, only the tile of nodes its rays can reach in
+//              the block's kb steps (|dx/ds| = 1, so within (kb + 1) ds of where
+//              they start), a few KB: the kernel is no longer capped at one
+//              workgroup per CU, and its waves share every SIMD with the alpha
+//              waves.  A stencil outside the tile reads the global array (the
+//              same values: results bit-identical in every mode).
+enum { kTrajL2 = 0, kTrajLds = 1, kTrajTile = 2 };
 constexpr int kTrajLdsNS = 6;
-template <int DEPO, bool TRAJ, bool LDS>
-__device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &sp) {
-    constexpr int NS = LDS ? kTrajLdsNS : kNF;
-    const double *coef = a.coef;
-    if constexpr (LDS) {
-        extern __shared__ double s_coef[];
-        const int nodes = (a.g.nR + 2) * (a.g.nZ + 2);
-        for (int k = threadIdx.x; k < nodes * kTrajLdsNS; k += blockDim.x)
-            s_coef[k] = a.coef[(size_t)(k / kTrajLdsNS) * kNF + k % kTrajLdsNS];
-        __syncthreads();
-        coef = s_coef;
-    }
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= a.n) return;
-    double x[3], N[3];
-    int steps, st;
-    if (sp.k0 == 0) {
+static_assert(kTrajLdsNS == kTileNS, "LDS layouts");
+#ifndef TORJ_TILE_NODES
+#define TORJ_TILE_NODES 256  // 12 KB of LDS per wave
+#endif
+constexpr int kTileNodes = TORJ_TILE_NODES;
+
+__device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
-        for (int c = 0; c < 3; c++) {
-            x[c] = a.x0[c * a.n + i];
-            N[c] = a.N0[c * a.n + i];
-            sp.cbx[c * (size_t)a.n + i] = x[c];
-            sp.cbx[(3 + c) * (size_t)a.n + i] = N[c];
-        }
-        steps = 0;
-        st = ST_OK;
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ double wave_max(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+    return v;
+}
+// the cell index axis_setup gives a coordinate (monotone in x)
+__device__ __forceinline__ int cell_index(double x, double x1, double xn, double invh, int n) {
+    const int i = (int)floor((clampd(x, x1, xn) - x1) * invh);
+    return i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+}
+
+// the trajectory steps of one ray over the block, from its carry (x, N, steps)
+template <int DEPO, bool TRAJ, int NS, class CS>
+__device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp, CS coef, int i,
+                                         double x[3], double N[3], int steps, int st) {
+    if (sp.k0 == 0) {
         if constexpr (DEPO != kDepoNone) {
             const double psi0 = eval_one<NS>(coef, a.g, sqrt(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
             sp.spsi[i] = psi0;  // the scan's psi_a at step 0
@@ -1006,24 +1018,7 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
                 a.smp_dpds[smp_at(0, i, a.smp_rows)] = 0.0;
             }
         }
-    } else {
-        const int v = sp.tinfo[i];
-        steps = info_steps(v);
-        st = info_status(v);
-#pragma unroll
-        for (int c = 0; c < 3; c++) {
-            x[c] = sp.tx[c * (size_t)a.n + i];
-            N[c] = sp.tx[(3 + c) * (size_t)a.n + i];
-        }
     }
-    // a ray the scan has stopped (ABSORBED) needs no more trajectory.  sinfo is
-    // written by k_tau_scan on another stream while this kernel may run, so the
-    // read can be stale.  INVARIANT: this early-out only saves work, it never
-    // decides an output -- a stale OK just traces steps nobody reads (the scan
-    // stopped first; k_split_final rebuilds the state from the chunk-boundary
-    // copy and the scan's carry).  Keep it that way: tests/test_gpu_split.py
-    // test_split_serial_equals_overlapped holds both orders bit-identical.
-    if (st != ST_OK || (sp.k0 > 0 && info_status(sp.sinfo[i]) != ST_OK)) return;
     const int s_end = min(a.n_steps, sp.k0 + sp.kb);
     for (int s = steps; s < s_end; s++) {
         double xn[3], Nn[3];
@@ -1073,16 +1068,100 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
     sp.tinfo[i] = make_info(steps, st);
 }
 
+
+template <int DEPO, bool TRAJ, int MODE>
+__device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &sp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    double x[3] = {0, 0, 0}, N[3] = {0, 0, 0};
+    int steps = 0, st = ST_OK;
+    bool live = i < a.n;
+    if (live) {
+        if (sp.k0 == 0) {
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                x[c] = a.x0[c * a.n + i];
+                N[c] = a.N0[c * a.n + i];
+                sp.cbx[c * (size_t)a.n + i] = x[c];
+                sp.cbx[(3 + c) * (size_t)a.n + i] = N[c];
+            }
+        } else {
+            const int v = sp.tinfo[i];
+            steps = info_steps(v);
+            st = info_status(v);
+#pragma unroll
+            for (int c = 0; c < 3; c++) {
+                x[c] = sp.tx[c * (size_t)a.n + i];
+                N[c] = sp.tx[(3 + c) * (size_t)a.n + i];
+            }
+        }
+        // a ray the scan has stopped (ABSORBED) needs no more trajectory.  sinfo is
+        // written by k_tau_scan on another stream while this kernel may run, so the
+        // read can be stale.  INVARIANT: this early-out only saves work, it never
+        // decides an output -- a stale OK just traces steps nobody reads (the scan
+        // stopped first; k_split_final rebuilds the state from the chunk-boundary
+        // copy and the scan's carry).  Keep it that way: tests/test_gpu_split.py
+        // test_split_serial_equals_overlapped holds both orders bit-identical.
+        live = st == ST_OK && !(sp.k0 > 0 && info_status(sp.sinfo[i]) != ST_OK);
+    }
+    if constexpr (MODE == kTrajTile) {
+        // one wave per workgroup: the wave's live rays' (R, Z) box, widened by
+        // the path the block can take, and its nodes staged in LDS
+        __shared__ double s_tile[kTileNodes * kTileNS];
+        const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
+        const double inf = __builtin_inf();
+        const double rmin = wave_min(live ? R : inf), rmax = wave_max(live ? R : -inf);
+        const double zmin = wave_min(live ? x[2] : inf), zmax = wave_max(live ? x[2] : -inf);
+        if (!(rmin <= rmax && zmin <= zmax)) return;  // no live ray in the wave (wave-uniform)
+        const double m = (double)(sp.kb + 1) * a.ds * sp.tile_margin;
+        const int iR0 = cell_index(rmin - m, a.g.R1, a.g.Rn, a.g.invhR, a.g.nR),
+                  iR1 = cell_index(rmax + m, a.g.R1, a.g.Rn, a.g.invhR, a.g.nR),
+                  iZ0 = cell_index(zmin - m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ),
+                  iZ1 = cell_index(zmax + m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ);
+        TileCoef tc{a.coef, s_tile, iR0, iZ0, iR1 - iR0 + 4, iZ1 - iZ0 + 4};
+        if (tc.tw * tc.th > sp.tile_cap) {
+            tc.tw = tc.th = 0;  // too wide for the tile: every stencil from global memory
+        } else {
+            const int mR = a.g.nR + 2, cnt = tc.tw * tc.th * kTileNS;
+            for (int k = threadIdx.x; k < cnt; k += 64) {
+                const int node = k / kTileNS, f = k - node * kTileNS;
+                const int zr = node / tc.tw, rr = node - zr * tc.tw;
+                s_tile[k] = a.coef[((size_t)(iZ0 + zr) * mR + iR0 + rr) * kNF + f];
+            }
+        }
+        __syncthreads();
+        if (!live) return;
+        traj_run<DEPO, TRAJ, kTileNS>(a, sp, tc, i, x, N, steps, st);
+    } else if constexpr (MODE == kTrajLds) {
+        extern __shared__ double s_coef[];
+        const int nodes = (a.g.nR + 2) * (a.g.nZ + 2);
+        for (int k = threadIdx.x; k < nodes * kTrajLdsNS; k += blockDim.x)
+            s_coef[k] = a.coef[(size_t)(k / kTrajLdsNS) * kNF + k % kTrajLdsNS];
+        __syncthreads();
+        if (!live) return;
+        traj_run<DEPO, TRAJ, kTrajLdsNS>(a, sp, (const double *)s_coef, i, x, N, steps, st);
+    } else {
+        if (!live) return;
+        traj_run<DEPO, TRAJ, kNF>(a, sp, (const double *)a.coef, i, x, N, steps, st);
+    }
+}
+
 template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_TRAJ_WAVES) k_traj(TraceArgs a, SplitArgs sp) {
-    traj_body<DEPO, TRAJ, false>(a, sp);
+    traj_body<DEPO, TRAJ, kTrajL2>(a, sp);
 }
 #ifndef TORJ_TRAJ_LDS_WAVES
 #define TORJ_TRAJ_LDS_WAVES 1
 #endif
 template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(512, TORJ_TRAJ_LDS_WAVES) k_traj_lds(TraceArgs a, SplitArgs sp) {
-    traj_body<DEPO, TRAJ, true>(a, sp);
+    traj_body<DEPO, TRAJ, kTrajLds>(a, sp);
+}
+#ifndef TORJ_TRAJ_TILE_WAVES
+#define TORJ_TRAJ_TILE_WAVES 2
+#endif
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_tile(TraceArgs a, SplitArgs sp) {
+    traj_body<DEPO, TRAJ, kTrajTile>(a, sp);
 }
 
 // alpha at the stored stage points of one block: block = 256 lanes = 4 groups
@@ -1420,13 +1499,20 @@ __device__ __forceinline__ bool fit_grid_lds(FitArgs &a) {
     a.grid = s_grid;
     return true;
 }
-__global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds, const int *sinfo) {
+// s_cap: the steps whose samples this launch may read (the end of the block
+// whose scan it follows).  On its own stream (TORJ_DEPO_STREAM=2) the launch
+// can overlap the next block's scan, so sinfo may already hold that scan's
+// carry, whose samples need not be visible yet: S is capped at the block end
+// (and a ray that scan stopped is left to k_depo_tail, as any stopped ray).
+// Windows are schedule-independent (torj_fitdepo.hpp), so the outputs do not
+// depend on which carry the read saw.
+__global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds, const int *sinfo, int s_cap) {
     fit_grid_lds(a);
     const int i = blockIdx.x * 64 + threadIdx.x;
     if (i >= a.n) return;
-    const int v = sinfo[i];
+    const int v = __hip_atomic_load(sinfo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (info_status(v) != ST_OK) return;  // stopped: k_depo_tail takes the rest
-    const int S = info_steps(v), j = ds.v[kDsJ * (size_t)a.n + i];
+    const int S = min(info_steps(v), s_cap), j = ds.v[kDsJ * (size_t)a.n + i];
     if ((j < 0 ? 0 : j) + kDepoQ + 3 + kDepoW > S) return;  // no new window yet
     // psi at the launch point (point 0) enters only the walk's start
     double psiL = 0.0;
@@ -1756,8 +1842,10 @@ struct torj_plasma_s {
     size_t split_cap = 0;
     hipStream_t stream2 = nullptr, streamT = nullptr;  // alpha; trajectory (high priority)
     hipStream_t streamS = nullptr;                      // optical-depth scan
+    hipStream_t streamD = nullptr;                      // streamed deposition windows (TORJ_DEPO_STREAM=2)
     static constexpr int kRing = 4;                     // alpha-input buffers in flight
     hipEvent_t ev_T[kRing] = {}, ev_A[kRing] = {}, ev_S[kRing] = {}, ev_J = nullptr, ev_F = nullptr;
+    hipEvent_t ev_D = nullptr;
 };
 
 static const int kFieldSlot[6] = {F_PSI, F_LNNE, F_LNTE, F_BR, F_BZ, F_BPHI};
@@ -1848,6 +1936,7 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
         HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
         HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
+        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, lo));
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
             HIPCK(hipEventCreateWithFlags(&p->ev_A[q], hipEventDisableTiming));
@@ -1855,6 +1944,7 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         }
         HIPCK(hipEventCreateWithFlags(&p->ev_J, hipEventDisableTiming));
         HIPCK(hipEventCreateWithFlags(&p->ev_F, hipEventDisableTiming));
+        HIPCK(hipEventCreateWithFlags(&p->ev_D, hipEventDisableTiming));
     }
     if (p->split_cap >= bytes) return 0;
     if (p->d_split) HIPCK(hipFree(p->d_split));
@@ -2102,9 +2192,11 @@ int torj_plasma_destroy(torj_plasma_t p) {
     }
     if (p->ev_J) (void)hipEventDestroy(p->ev_J);
     if (p->ev_F) (void)hipEventDestroy(p->ev_F);
+    if (p->ev_D) (void)hipEventDestroy(p->ev_D);
     if (p->stream2) (void)hipStreamDestroy(p->stream2);
     if (p->streamT) (void)hipStreamDestroy(p->streamT);
     if (p->streamS) (void)hipStreamDestroy(p->streamS);
+    if (p->streamD) (void)hipStreamDestroy(p->streamD);
     delete p;
     return 0;
 }
@@ -2261,6 +2353,20 @@ struct DevBufs {
         ptrs.push_back((void *)q);
         return q;
     }
+    // dupload / dalloc whose buffer is owned from the moment it exists (freed
+    // on every early return, a failed copy after a good allocation included)
+    template <typename T>
+    int up(T **d, const T *h, size_t n, hipStream_t s) {
+        const int r = dupload(d, h, n, s);
+        track(*d);
+        return r;
+    }
+    template <typename T>
+    int alloc(T **d, size_t n, bool want) {
+        const int r = dalloc(d, n, want);
+        track(*d);
+        return r;
+    }
 };
 
 static inline int nblocks(int n, int b) { return (n + b - 1) / b; }
@@ -2274,10 +2380,9 @@ int torj_eval_plasma(torj_plasma_t p, int n, const double *x, const double *N, d
     if (ensure_device(p)) return -1;
     DevBufs B;
     double *dx, *dN, *dout;
-    if (dupload(&dx, x, 3 * (size_t)n, p->stream) || dupload(&dN, N, 3 * (size_t)n, p->stream) ||
-        dalloc(&dout, 13 * (size_t)n, true))
+    if (B.up(&dx, x, 3 * (size_t)n, p->stream) || B.up(&dN, N, 3 * (size_t)n, p->stream) ||
+        B.alloc(&dout, 13 * (size_t)n, true))
         return -1;
-    B.track(dx), B.track(dN), B.track(dout);
     EvalArgs a{};
     a.coef = p->d_coef;
     a.g = p->g;
@@ -2302,11 +2407,10 @@ int torj_dispersion(torj_plasma_t p, int n, const double *x, const double *N, do
     if (alpha && ensure_gl_on_device(p->device)) return -1;
     DevBufs B;
     double *dx, *dN, *dD, *ddu, *dal;
-    if (dupload(&dx, x, 3 * (size_t)n, p->stream) || dupload(&dN, N, 3 * (size_t)n, p->stream) ||
-        dalloc(&dD, n, D != nullptr) || dalloc(&ddu, 6 * (size_t)n, du != nullptr) ||
-        dalloc(&dal, n, alpha != nullptr))
+    if (B.up(&dx, x, 3 * (size_t)n, p->stream) || B.up(&dN, N, 3 * (size_t)n, p->stream) ||
+        B.alloc(&dD, n, D != nullptr) || B.alloc(&ddu, 6 * (size_t)n, du != nullptr) ||
+        B.alloc(&dal, n, alpha != nullptr))
         return -1;
-    B.track(dx), B.track(dN), B.track(dD), B.track(ddu), B.track(dal);
     EvalArgs a{};
     a.coef = p->d_coef;
     a.g = p->g;
@@ -2346,11 +2450,9 @@ static int batched_scalar(bool albajar, int n, const double *omega, const double
     const double *h[6] = {omega, X, Y, Nabs, Npar, Te};
     for (int k = 0; k < 6; k++) {
         d[k] = nullptr;
-        if (h[k] && dupload(&d[k], h[k], n, nullptr)) return -1;
-        B.track(d[k]);
+        if (h[k] && B.up(&d[k], h[k], n, nullptr)) return -1;
     }
-    if (dalloc(&d[6], n, true)) return -1;
-    B.track(d[6]);
+    if (B.alloc(&d[6], n, true)) return -1;
     a.omega = d[0], a.X = d[1], a.Y = d[2], a.Nabs = d[3], a.Npar = d[4], a.Te = d[5];
     a.out = d[6];
     if (albajar)
@@ -2383,11 +2485,9 @@ int torj_alpha_warm(int n, const double *omega, const double *X, const double *Y
     const double *h[7] = {omega, X, Y, Nabs, Npar, Te, inv_dDdN};
     for (int k = 0; k < 7; k++) {
         if (!h[k]) return fail("torj_alpha_warm: every input array is required");
-        if (dupload(&d[k], h[k], n, nullptr)) return -1;
-        B.track(d[k]);
+        if (B.up(&d[k], h[k], n, nullptr)) return -1;
     }
-    if (dalloc(&d[7], n, true) || dalloc(&d[8], 2 * (size_t)n, true)) return -1;
-    B.track(d[7]), B.track(d[8]);
+    if (B.alloc(&d[7], n, true) || B.alloc(&d[8], 2 * (size_t)n, true)) return -1;
     a.omega = d[0], a.X = d[1], a.Y = d[2], a.Nabs = d[3], a.Npar = d[4], a.Te = d[5];
     a.inv = d[6], a.out = d[7], a.n2 = d[8];
     hipLaunchKernelGGL(k_alpha_warm, dim3(nblocks(n, 64)), dim3(64), 0, nullptr, a);
@@ -2423,12 +2523,10 @@ int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N
     DevBufs B;
     double *dx0, *dN0, *dxp, *dNp, *ds0;
     int *dst;
-    if (dupload(&dx0, x0, 3 * (size_t)n, s) || dupload(&dN0, N0, 3 * (size_t)n, s)) return -1;
-    B.track(dx0), B.track(dN0);
-    if (dalloc(&dxp, 3 * (size_t)n, true) || dalloc(&dNp, 3 * (size_t)n, true) ||
-        dalloc(&ds0, n, true) || dalloc(&dst, n, true))
+    if (B.up(&dx0, x0, 3 * (size_t)n, s) || B.up(&dN0, N0, 3 * (size_t)n, s)) return -1;
+    if (B.alloc(&dxp, 3 * (size_t)n, true) || B.alloc(&dNp, 3 * (size_t)n, true) ||
+        B.alloc(&ds0, n, true) || B.alloc(&dst, n, true))
         return -1;
-    B.track(dxp), B.track(dNp), B.track(ds0), B.track(dst);
     if (torj_ray_entry_device(p, n, dx0, dN0, omega, mode, dxp, dNp, ds0, dst, s)) return -1;
     if (ddownload(xp, dxp, 3 * (size_t)n, s) || ddownload(Np, dNp, 3 * (size_t)n, s) ||
         ddownload(s0, ds0, n, s) || ddownload(status, dst, n, s))
@@ -2478,6 +2576,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int nq = (int)((n + 255) / 256);
     // the streamed deposition's per-ray walk state (fa: the reference profile;
     // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
+    // TORJ_DEPO_STREAM=1: the windows on the scan's stream, after each scan;
+    // =2: on a stream of their own, each after its block's scan, so the next
+    // scan (and the ring slot it releases) does not wait behind them
     const char *dstream_e = getenv("TORJ_DEPO_STREAM");  // read per call (tests compare both)
     const int dstream_env = dstream_e ? atoi(dstream_e) : 1;
     const bool dstream = fa && dso && dstream_env != 0;
@@ -2534,6 +2635,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     }();
     hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
     hipStream_t s3 = serial ? s : (scan_own ? p->streamS : p->stream2);
+    const bool depo_own = dstream && dstream_env == 2 && !serial;
+    hipStream_t sD = depo_own ? p->streamD : s3;
     if (!serial) {  // fork from the caller's stream
         HIPCK(hipEventRecord(p->ev_F, s));
         HIPCK(hipStreamWaitEvent(sT, p->ev_F, 0));
@@ -2550,12 +2653,16 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // fits 160 KiB at 6 fp64 per node (56 x 56: 161 KB), one workgroup of wpb
     // waves per CU (measured: trajectory kernel 28.2 -> 24.3 ms, pipeline 67.2 ->
     // 61.6 ms on the headline beam; TORJ_TRAJ_LDS=0 reads them through L2)
-    static const int lds_env = [] {
-        const char *e = getenv("TORJ_TRAJ_LDS");
-        return e ? atoi(e) : 1;
-    }();
+    // (read per call: the tests compare the modes; TORJ_TILE_CAP / TORJ_TILE_MARGIN
+    // shrink the tile to exercise the global-memory fallback)
+    const char *lds_e = getenv("TORJ_TRAJ_LDS");
+    const int lds_env = lds_e ? atoi(lds_e) : 1;
+    const char *cap_e = getenv("TORJ_TILE_CAP"), *mar_e = getenv("TORJ_TILE_MARGIN");
+    sp.tile_cap = std::min(kTileNodes, cap_e ? atoi(cap_e) : kTileNodes);
+    sp.tile_margin = mar_e ? atof(mar_e) : 1.001;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
     const bool lds_traj = lds_env == 1 && lds_bytes <= 160 * 1024;
+    const bool tile_traj = lds_env == 2;
     const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
@@ -2581,7 +2688,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
-        if (lds_traj)
+        if (tile_traj)
+            TORJ_SPLIT_DISPATCH(k_traj_tile, dim3(G), dim3(64), 0, sT, a, sp);
+        else if (lds_traj)
             TORJ_SPLIT_DISPATCH(k_traj_lds, dim3(nblocks(G, wpb)), dim3(64 * wpb), lds_bytes, sT, a, sp);
         else
             TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
@@ -2608,7 +2717,11 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         // (measured on the headline beam: after every block on the scan's stream
         // 3.62-3.63e9 ray-steps/s; every 2nd / 4th block 3.45-3.64 / 3.58-3.59e9;
         // behind the alpha or the trajectory kernel's stream 3.03 / 2.98e9)
-        if (dstream && b + 1 < n_blocks) hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, s3, *fa, ds, sp.sinfo);
+        if (dstream && b + 1 < n_blocks) {
+            if (depo_own) HIPCK(hipStreamWaitEvent(sD, p->ev_S[r], 0));
+            hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
+                               sp.k0 + sp.kb);
+        }
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
 #undef TORJ_SPLIT_DISPATCH
@@ -2616,6 +2729,10 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                     // and each alpha kernel its trajectory
         HIPCK(hipEventRecord(p->ev_J, s3));
         HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
+        if (depo_own) {
+            HIPCK(hipEventRecord(p->ev_D, sD));
+            HIPCK(hipStreamWaitEvent(s, p->ev_D, 0));
+        }
     }
     HIPCK(hipGetLastError());
     return 0;
@@ -3076,14 +3193,12 @@ int torj_power_deposition_profile(torj_plasma_t p, int n_rays, const int *n_poin
     double *d_s, *d_x, *d_dp, *d_grid, *d_smp, *d_Pr;
     int *d_np, *d_kstar, *d_cnt;
     long *d_off;
-    if (dupload(&d_s, s, (size_t)tot, st) || dupload(&d_x, x, 3 * (size_t)tot, st) ||
-        dupload(&d_dp, dP_ds, (size_t)tot, st) || dupload(&d_grid, grid, L, st) ||
-        dupload(&d_np, n_points, N, st) || dupload(&d_off, off.data(), N, st) ||
-        dalloc(&d_smp, 6 * KN + 2 * L * N, true) || dalloc(&d_cnt, (L + 1) * N, true) ||
-        dalloc(&d_kstar, N, true) || dalloc(&d_Pr, N, true))
+    if (B.up(&d_s, s, (size_t)tot, st) || B.up(&d_x, x, 3 * (size_t)tot, st) ||
+        B.up(&d_dp, dP_ds, (size_t)tot, st) || B.up(&d_grid, grid, L, st) ||
+        B.up(&d_np, n_points, N, st) || B.up(&d_off, off.data(), N, st) ||
+        B.alloc(&d_smp, 6 * KN + 2 * L * N, true) || B.alloc(&d_cnt, (L + 1) * N, true) ||
+        B.alloc(&d_kstar, N, true) || B.alloc(&d_Pr, N, true))
         return -1;
-    B.track(d_s), B.track(d_x), B.track(d_dp), B.track(d_grid), B.track(d_np), B.track(d_off);
-    B.track(d_smp), B.track(d_cnt), B.track(d_kstar), B.track(d_Pr);
     FitArgs fa{};
     fa.coef = p->d_coef;
     fa.g = p->g;
@@ -3121,7 +3236,7 @@ int torj_power_deposition_profile(torj_plasma_t p, int n_rays, const int *n_poin
     // dP_dV[j] = dP_j / (V(psi_{j+1}) - V(psi_j)) above the break shell, 0 below it
     // and at the last boundary (src/plasma.jl:141)
     std::vector<double> dV(L - 1);
-    torj_shell_volumes(p, n_psi, grid, dV.data());
+    if (torj_shell_volumes(p, n_psi, grid, dV.data())) return -1;
     for (size_t r = 0; r < N; r++) {
         double *row = dP_dV + r * L;
         for (size_t j = 0; j < L; j++)
@@ -3191,35 +3306,28 @@ int torj_trace_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const doubl
     double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dstate, *ddP = nullptr, *dPdep = nullptr,
                                 *dtraj = nullptr;
     int *dstatus, *dsteps;
-    if (dupload(&dx0, x0, 3 * (size_t)n, s) || dupload(&dN0, N0, 3 * (size_t)n, s)) return -1;
-    B.track(dx0), B.track(dN0);
+    if (B.up(&dx0, x0, 3 * (size_t)n, s) || B.up(&dN0, N0, 3 * (size_t)n, s)) return -1;
     if (weights) {
-        if (dupload(&dw, weights, n, s)) return -1;
-        B.track(dw);
+        if (B.up(&dw, weights, n, s)) return -1;
     }
     if (depo) {
-        if (dupload(&dgrid, grid, n_psi, s) || dalloc(&ddP, n_psi + 1, true) ||
-            dalloc(&dPdep, n, true))
+        if (B.up(&dgrid, grid, n_psi, s) || B.alloc(&ddP, n_psi + 1, true) ||
+            B.alloc(&dPdep, n, true))
             return -1;
-        B.track(dgrid), B.track(ddP), B.track(dPdep);
         HIPCK(hipMemsetAsync(ddP, 0, (n_psi + 1) * sizeof(double), s));
     }
-    if (dalloc(&dstate, 7 * (size_t)n, true) || dalloc(&dstatus, n, true) ||
-        dalloc(&dsteps, n, true))
+    if (B.alloc(&dstate, 7 * (size_t)n, true) || B.alloc(&dstatus, n, true) ||
+        B.alloc(&dsteps, n, true))
         return -1;
-    B.track(dstate), B.track(dstatus), B.track(dsteps);
     if (traj && n_save > 0) {
-        if (dalloc(&dtraj, (size_t)n_save * 5 * n, true)) return -1;
-        B.track(dtraj);
+        if (B.alloc(&dtraj, (size_t)n_save * 5 * n, true)) return -1;
     }
     double *dxl = nullptr, *ds0 = nullptr;
     if (x_launch) {
-        if (dupload(&dxl, x_launch, 3 * (size_t)n, s)) return -1;
-        B.track(dxl);
+        if (B.up(&dxl, x_launch, 3 * (size_t)n, s)) return -1;
     }
     if (s0) {
-        if (dupload(&ds0, s0, n, s)) return -1;
-        B.track(ds0);
+        if (B.up(&ds0, s0, n, s)) return -1;
     }
     if (torj_trace_device_ex(p, cfg, n, dx0, dN0, dw, depo ? n_psi : 0, dgrid, dxl, ds0, dstate,
                              dstatus, dsteps, ddP, dPdep, dtraj, nullptr, s))
@@ -3397,17 +3505,14 @@ static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S
     double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dxl = nullptr, *ds0 = nullptr, *dstate,
                        *dPdep = nullptr, *dtraj = nullptr;
     int *dstatus, *dsteps;
-    if (dalloc(&dx0, 3 * (size_t)m, true) || dalloc(&dN0, 3 * (size_t)m, true) ||
-        dalloc(&dstate, 7 * (size_t)m, true) || dalloc(&dstatus, m, true) || dalloc(&dsteps, m, true) ||
-        dalloc(&dw, m, w != nullptr) || dalloc(&dxl, 3 * (size_t)m, xl != nullptr) ||
-        dalloc(&ds0, m, s0 != nullptr) || dalloc(&dPdep, m, depo) ||
-        dalloc(&dtraj, (size_t)n_save * 5 * m, traj && n_save > 0))
+    if (B.alloc(&dx0, 3 * (size_t)m, true) || B.alloc(&dN0, 3 * (size_t)m, true) ||
+        B.alloc(&dstate, 7 * (size_t)m, true) || B.alloc(&dstatus, m, true) || B.alloc(&dsteps, m, true) ||
+        B.alloc(&dw, m, w != nullptr) || B.alloc(&dxl, 3 * (size_t)m, xl != nullptr) ||
+        B.alloc(&ds0, m, s0 != nullptr) || B.alloc(&dPdep, m, depo) ||
+        B.alloc(&dtraj, (size_t)n_save * 5 * m, traj && n_save > 0))
         return -1;
-    B.track(dx0), B.track(dN0), B.track(dstate), B.track(dstatus), B.track(dsteps), B.track(dw);
-    B.track(dxl), B.track(ds0), B.track(dPdep), B.track(dtraj);
     if (depo) {
-        if (dupload(&dgrid, grid, n_psi, s)) return -1;
-        B.track(dgrid);
+        if (B.up(&dgrid, grid, n_psi, s)) return -1;
     }
     const size_t D = sizeof(double);
     // rows x cnt sub-block of a (rows x n) SoA host array <-> compact (rows x cnt) device array

@@ -233,22 +233,23 @@ struct FieldPack {
 // point is inside the grid on both axes (Line() extrapolation distances 0) and
 // skips the sums only the extrapolation needs (value-only fields' slopes, the
 // mixed derivative); the results are then identical to EXT = true.
-template <int NGRAD, int NVAL, bool EXT = true, int NS = kNF>
-TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double R, double Z,
-                         const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
+// The 4 x 4 stencil's tensor-product sums from the node at `c0` (the stencil's
+// first node), `rs` doubles between rows of nodes, NS doubles per node,
+// accumulated row by row (few live registers):
+//   v = sum wZ wR c, gr = sum wZ dwR c, gz = sum dwZ wR c, grz = sum dwZ dwR c
+// The same arithmetic whatever memory c0 points into (global / L2 or an LDS
+// tile), so the results do not depend on where the coefficients were read.
+template <int NGRAD, int NVAL, bool EXT, int NS, class P = const double *>
+TORJ_HD void stencil_sums(P c0, int rs, const Axis &aR, const Axis &aZ,
+                          const int (&fidx)[NGRAD + NVAL], double (&v)[NGRAD + NVAL],
+                          double (&gr)[NGRAD + NVAL], double (&gz)[NGRAD + NVAL],
+                          double (&grz)[NGRAD + NVAL]) {
     constexpr int NT = NGRAD + NVAL;
-    Axis aR, aZ;
-    axis_setup(R, g.R1, g.Rn, g.invhR, g.nR, aR);
-    axis_setup(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
-    const int mR = g.nR + 2;
-    // tensor-product sums accumulated row by row (few live registers):
-    //   v = sum wZ wR c, gr = sum wZ dwR c, gz = sum dwZ wR c, grz = sum dwZ dwR c
-    double v[NT], gr[NT], gz[NT], grz[NT];
 #pragma unroll
     for (int f = 0; f < NT; f++) v[f] = gr[f] = gz[f] = grz[f] = 0.0;
 #pragma unroll
     for (int b = 0; b < 4; b++) {
-        const double *row = coef + ((size_t)(aZ.i + b) * mR + aR.i) * NS;
+        const P row = c0 + (size_t)b * rs;
 #pragma unroll
         for (int f = 0; f < NT; f++) {
             const bool slopes = EXT || f < NGRAD;
@@ -267,6 +268,78 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
             if (EXT && f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
         }
     }
+}
+
+// A wave's tile of the coefficient grid staged in LDS (the split pipeline's
+// trajectory kernel): nodes [iR0, iR0 + tw) x [iZ0, iZ0 + th)
+// at kTileNS doubles per node, R fastest; `g` is the whole grid (kNF per node)
+// for a stencil that leaves the tile.  tw = 0: no tile, every read from g.
+constexpr int kTileNS = 6;
+struct TileCoef {
+    const double *g;    // global coefficients, kNF doubles per node
+    const double *lds;  // the tile
+    int iR0, iZ0, tw, th;
+};
+
+template <int NGRAD, int NVAL, bool EXT>
+TORJ_HD void fields_finish(const Grid &g, const Axis &aR, const Axis &aZ, const double *v,
+                           const double *gr, const double *gz, const double *grz,
+                           FieldPack<NGRAD, NVAL> &out);
+
+// eval_fields reading the stencil from the wave's LDS tile when every lane's
+// stencil lies inside it (one wave-uniform branch), from global memory
+// otherwise; bit-identical to eval_fields on the whole grid either way.
+template <int NGRAD, int NVAL, bool EXT = true, int NS = kNF>
+TORJ_HD void eval_fields(const TileCoef &t, const Grid &g, double R, double Z,
+                         const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
+    constexpr int NT = NGRAD + NVAL;
+    Axis aR, aZ;
+    axis_setup(R, g.R1, g.Rn, g.invhR, g.nR, aR);
+    axis_setup(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
+    const int dR = aR.i - t.iR0, dZ = aZ.i - t.iZ0;
+    bool in = dR >= 0 && dR <= t.tw - 4 && dZ >= 0 && dZ <= t.th - 4;
+#ifdef __HIP_DEVICE_COMPILE__
+    in = __all(in);
+#endif
+    double v[NT], gr[NT], gz[NT], grz[NT];
+#ifdef __HIP_DEVICE_COMPILE__
+    // explicit address spaces: ds_read from the tile, global_load otherwise (as
+    // generic pointers the two paths merge into one flat load of either)
+    using LdsP = const __attribute__((address_space(3))) double *;
+    using GlbP = const __attribute__((address_space(1))) double *;
+#else
+    using LdsP = const double *;
+    using GlbP = const double *;
+#endif
+    if (in)
+        stencil_sums<NGRAD, NVAL, EXT, kTileNS, LdsP>((LdsP)t.lds + ((size_t)dZ * t.tw + dR) * kTileNS,
+                                                      t.tw * kTileNS, aR, aZ, fidx, v, gr, gz, grz);
+    else
+        stencil_sums<NGRAD, NVAL, EXT, kNF, GlbP>((GlbP)t.g + ((size_t)aZ.i * (g.nR + 2) + aR.i) * kNF,
+                                                  (g.nR + 2) * kNF, aR, aZ, fidx, v, gr, gz, grz);
+    fields_finish<NGRAD, NVAL, EXT>(g, aR, aZ, v, gr, gz, grz, out);
+}
+
+template <int NGRAD, int NVAL, bool EXT = true, int NS = kNF>
+TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double R, double Z,
+                         const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
+    constexpr int NT = NGRAD + NVAL;
+    Axis aR, aZ;
+    axis_setup(R, g.R1, g.Rn, g.invhR, g.nR, aR);
+    axis_setup(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
+    const int mR = g.nR + 2;
+    double v[NT], gr[NT], gz[NT], grz[NT];
+    stencil_sums<NGRAD, NVAL, EXT, NS>(coef + ((size_t)aZ.i * mR + aR.i) * NS, mR * NS, aR, aZ, fidx,
+                                       v, gr, gz, grz);
+    fields_finish<NGRAD, NVAL, EXT>(g, aR, aZ, v, gr, gz, grz, out);
+}
+
+// physical gradients and Line() extrapolation from the stencil sums
+template <int NGRAD, int NVAL, bool EXT>
+TORJ_HD void fields_finish(const Grid &g, const Axis &aR, const Axis &aZ, const double *v,
+                           const double *gr, const double *gz, const double *grz,
+                           FieldPack<NGRAD, NVAL> &out) {
+    constexpr int NT = NGRAD + NVAL;
     const bool outR = aR.delta != 0.0, outZ = aZ.delta != 0.0;
 #pragma unroll
     for (int f = 0; f < NT; f++) {
@@ -302,8 +375,8 @@ TORJ_HD bool inside_grid(const Grid &g, double R, double Z) {
 }
 
 // single value (e.g. psi for termination / deposition)
-template <int NS = kNF>
-TORJ_HD double eval_one(const double *__restrict__ coef, const Grid &g, double R, double Z, int field) {
+template <int NS = kNF, class CS = const double *>
+TORJ_HD double eval_one(CS coef, const Grid &g, double R, double Z, int field) {
     FieldPack<0, 1> p;
     const int idx[1] = {field};
     if (inside_grid(g, R, Z))
@@ -396,8 +469,8 @@ TORJ_HD Consts make_consts(double omega) {
 }
 
 // fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te
-template <bool WITH_TE, int NS = kNF>
-TORJ_HD void plasma_point(const double *__restrict__ coef, const Grid &g, const Consts &k,
+template <bool WITH_TE, int NS = kNF, class CS = const double *>
+TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
     const double R = sqrt_pos(x[0] * x[0] + x[1] * x[1]);
     const double invR = rcp_nz(R);
