@@ -60,6 +60,7 @@ void wh_albajar(int n, const double *om, const double *X, const double *Y, const
             g_wh_gl.w[i] = i < ngl ? w[i] : 0.0;
             g_wh_gl.st[i] = i < ngl ? sqrt(1.0 - t[i] * t[i]) : 0.0;
             g_wh_gl.t2[i] = i < ngl ? t[i] * t[i] : 0.0;
+            if (i < ngl) torj::gl_node_consts(g_wh_gl, i);
         }
     });
     for (int i = 0; i < n; i++)

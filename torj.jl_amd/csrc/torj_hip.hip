@@ -2102,6 +2102,7 @@ int torj_abs_al_init(int n) {
     for (int i = 0; i < n; i++) {
         t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);
         t.t2[i] = t.t[i] * t.t[i];
+        gl_node_consts(t, i);
     }
     g_gl_host = t;
     g_gl_version++;

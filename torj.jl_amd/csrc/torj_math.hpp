@@ -593,7 +593,18 @@ struct GLTable {
     int n;
     int negl_skip;  // 1: skip harmonic integrals provably below an ulp of the sum (default)
     double t[kMaxGL], w[kMaxGL], st[kMaxGL], t2[kMaxGL];  // nodes, weights, sqrt(1-t^2), t^2
+    // the node loop's per-node constants (pair_term): s2 = 1 - t^2 and the
+    // weights with the Bessel argument's node factor folded in, wm[m-2] = w s2^m
+    double s2[kMaxGL], wm[2][kMaxGL];
 };
+// s2 and wm of node i from its t and w (host, at abs_Al_init), in long double
+// so that each folded weight is rounded once
+inline void gl_node_consts(GLTable &g, int i) {
+    const long double t = g.t[i], s2 = 1.0L - t * t, w = g.w[i];
+    g.s2[i] = (double)s2;
+    g.wm[0][i] = (double)(w * s2 * s2);
+    g.wm[1][i] = (double)(w * s2 * s2 * s2);
+}
 
 #ifndef TORJ_ALBAJAR_NOINLINE
 #define TORJ_ALBAJAR_NOINLINE 1
@@ -650,6 +661,7 @@ struct HarmConst {
     double mu2;  // mu log2(e): the node exponent in base 2 (exp2_node)
     // node-pair form: gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
     double C0, C1, C2, hx;
+    double hx2, K1h, K5h;  // hx^2, K1 / hx = 2 Axz ea / m, K5 / hx = 2 q ea e3 / m (pair_term)
 };
 
 // A symmetric pair of Gauss-Legendre nodes (+t, -t): w * pol_fact * exp(mu (1 -
@@ -706,39 +718,41 @@ struct SeriesCoefs {
 //   gamma(+-t)^2 = (u_par0 +- u_par1 t)^2 + 1 + (r^2-1)(1-t^2) = C0 + C1 t^2 +- C2 t
 // the pair contributes w h^(2m-1) [P (E+ + E-) + t Q (E+ - E-)], E = exp(mu (1 - gamma))
 // -- the same sum as abs_Al_pol_fact x abs_Al_integral_nume_fast's node terms
-// (src/absorption.jl:132-189), regrouped.
+// (src/absorption.jl:132-189), regrouped.  With h = hx st (st = sqrt(1 - t^2)),
+// A = h S_m^2, B = K2 h^2 S_{m-1} h S_{m+1}, Cc = st S_m D = (h / hx) S_m D,
+// D = S_{m-1} - h^2 S_{m+1}, every term of P and Q carries one factor h, so
+//   w h^(2m-1) [..] = hx^(2m) (w s2^m) [P' (E+ + E-) + t Q' (E+ - E-)],
+//   P' = S_m^2 (K0 + K3 t^2) - K2 S_{m-1} u + (K1 / hx) S_m D,  u = h^2 S_{m+1},
+//   Q' = K4 S_m^2 + (K5 / hx) S_m D,
+// with s2 = 1 - t^2 and w s2^m per node (GLTable), K1 / hx and K5 / hx per
+// harmonic (no quotient: K1 and K5 carry a factor x_m = 2 hx), and hx^(2m)
+// applied once to the sum (albajar_harmonic): 25 VALU per pair besides the
+// series, square roots and exponentials, against 34 for the direct form.
+template <int M>
+TORJ_HD double gl_wm(const GLTable &gl, int i) {
+    static_assert(M == 2 || M == 3, "the Albajar sum has harmonics 2 and 3");
+    return gl.wm[M - 2][i];
+}
+
 template <int M, int LV>
-TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double st,
-                         double w, double t2, bool single) {
+TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double s2,
+                         double W, double t2, bool single) {
     constexpr double md = (double)M;
-    const double h = c.hx * st;  // half the Bessel argument x_m sqrt(1 - t^2)
-    const double h2 = h * h;
+    const double h2 = c.hx2 * s2;  // (x_m sqrt(1 - t^2) / 2)^2, the series' -z
     double Sm, Sm1;
     sc.eval(-h2, Sm, Sm1);
-    const double Sl = fma(-h2, Sm1, md * Sm);  // S_{m-1} by the downward recurrence
-    double p = h;  // h^(2m-1): h^3 = h^2 h, h^5 = (h^2 h^2) h
-    if constexpr (M == 2) {
-        p = h2 * h;
-    } else if constexpr (M == 3) {
-        p = (h2 * h2) * h;
-    } else {
-#pragma unroll
-        for (int k = 1; k < 2 * M - 1; k++) p *= h;
-    }
-    const double hSm = h * Sm;
-    const double A = hSm * Sm;
-    const double T1 = h2 * Sm1;
-    const double B = c.K2 * Sl * (h * T1);
-    const double Cc = st * Sm * (Sl - T1);
-    const double P = fma(A, fma(c.K3, t2, c.K0), fma(Cc, c.K1, -B));
-    const double wp = w * p;
+    const double u = h2 * Sm1;
+    const double Sl = fma(md, Sm, -u);  // S_{m-1} by the downward recurrence
+    const double D = Sl - u;
+    const double Sm2 = Sm * Sm, SmD = Sm * D;
+    const double P = fma(Sm2, fma(c.K3, t2, c.K0), fma(c.K1h, SmD, -(c.K2 * (Sl * u))));
     const double a = fma(c.C1, t2, c.C0);
-    if (single) return wp * P * exp2_node(fma(-c.mu2, sqrt_node(a), c.mu2));
-    const double Q = fma(A, c.K4, Cc * c.K5);
+    if (single) return W * (P * exp2_node(fma(-c.mu2, sqrt_node(a), c.mu2)));
+    const double Q = fma(c.K4, Sm2, c.K5h * SmD);
     const double b = c.C2 * t;
     const double Ep = exp2_node(fma(-c.mu2, sqrt_node(a + b), c.mu2));
     const double Em = exp2_node(fma(-c.mu2, sqrt_node(a - b), c.mu2));
-    return wp * fma(P, Ep + Em, (t * Q) * (Ep - Em));
+    return W * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 
 template <int M, int LV, int LPR = 1, int U = TORJ_PAIR_UNROLL>
@@ -760,7 +774,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
             rr[q] = 0.0;
             const int i = q * LPR + sub;
             if (q * LPR < half && i < half)
-                rr[q] = pair_term<M, LV>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
+                rr[q] = pair_term<M, LV>(c, sc, gl.t[i], gl.s2[i], gl_wm<M>(gl, i), gl.t2[i], false);
         }
         const int base = (int)(threadIdx.x & 63u) & ~(LPR - 1);
         double s = 0.0;
@@ -773,7 +787,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
                 if (q * LPR + u < half) s += v;
             }
         }
-        if (n & 1) s += pair_term<M, LV>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
+        if (n & 1) s += pair_term<M, LV>(c, sc, gl.t[half], gl.s2[half], gl_wm<M>(gl, half), gl.t2[half], true);
         return s;
     }
 #endif
@@ -788,8 +802,8 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
 #pragma unroll
     for (int u = 0; u < U; u++) {
         tn[u] = gl.t[u];
-        sn[u] = gl.st[u];
-        wn[u] = gl.w[u];
+        sn[u] = gl.s2[u];
+        wn[u] = gl_wm<M>(gl, u);
         qn[u] = gl.t2[u];
     }
     int i = 0;
@@ -803,8 +817,8 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
             w[u] = wn[u];
             q[u] = qn[u];
             tn[u] = gl.t[i + U + u];
-            sn[u] = gl.st[i + U + u];
-            wn[u] = gl.w[i + U + u];
+            sn[u] = gl.s2[i + U + u];
+            wn[u] = gl_wm<M>(gl, i + U + u);
             qn[u] = gl.t2[i + U + u];
         }
         double r[U];
@@ -821,8 +835,8 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, gl.t[i], gl.st[i], gl.w[i], gl.t2[i], false);
-    if (n & 1) acc[0] += pair_term<M, LV>(c, sc, gl.t[half], gl.st[half], gl.w[half], gl.t2[half], true);
+    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, gl.t[i], gl.s2[i], gl_wm<M>(gl, i), gl.t2[i], false);
+    if (n & 1) acc[0] += pair_term<M, LV>(c, sc, gl.t[half], gl.s2[half], gl_wm<M>(gl, half), gl.t2[half], true);
     double s = acc[0];
 #pragma unroll
     for (int u = 1; u < U; u++) s += acc[u];
@@ -899,6 +913,8 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     c.K3 = q * q * e3 * e3;
     c.K4 = 2.0 * q * Axz * e3;
     c.K5 = q * ea * e3 * c.x_m * inv_md;
+    c.K1h = 2.0 * Axz * ea * inv_md;     // K1 / hx
+    c.K5h = 2.0 * q * ea * e3 * inv_md;  // K5 / hx
     c.upa0 = hg.upa0;
     c.upa1 = hg.upa1;
     c.mu = mu;
@@ -907,6 +923,7 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     c.C1 = hg.C1;
     c.C2 = hg.C2;
     c.hx = 0.5 * c.x_m;
+    c.hx2 = c.hx * c.hx;
     const double qmin = hg.qmin;
     const bool zero = hg.zero;  // the exact-zero bound (harm_geom)
     // Bessel polynomial from the largest argument x_m (SeriesCoefs: x_m <= 1,
@@ -967,6 +984,11 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
         case 3: sum = node_sum<M, 3, LPR, U>(gl, c, sub); break;
         default: sum = node_sum<M, 4, LPR, U>(gl, c, sub); break;
     }
+    // hx^(2m), the node loop's common factor (pair_term)
+    double hx2m = c.hx2;
+#pragma unroll
+    for (int k = 1; k < M; k++) hx2m *= c.hx2;
+    sum *= hx2m;
     // (m / (N_perp omega_bar))^2 with Pm from a reciprocal (<= 1 ulp); N_perp = 0
     // (parallel propagation) stays an infinity as in the reference's quotient
     return -mu * Pm * Pm * sum * sq_r;
