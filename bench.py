@@ -81,9 +81,14 @@ def parse():
                          "for the ~1e6-ray beam over 8 GPUs")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-api", action="store_true",
-                    help="skip the host-pointer (PCIe-inclusive) call (profiling passes)")
+                    help="skip the host-pointer (PCIe-inclusive) calls and the library-path rate "
+                         "(profiling passes)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
+    ap.add_argument("--no-beam-host", action="store_true",
+                    help="skip the C4-scale torj_trace_beam host-pointer call (N = 1)")
+    ap.add_argument("--parity-rays", type=int, default=128,
+                    help="N > 1: rays of the oracle parity sample on rank 0 / device 0's shard")
     return ap.parse_args()
 
 
@@ -232,7 +237,27 @@ def main():
     tot_steps = torch.tensor([ray_steps_local], dtype=torch.float64, device=dev)
     el = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     km = torch.tensor([kern_ms, post_ms, hot_ms], dtype=torch.float64, device=dev)
+    per_rank = None
     if world > 1:
+        # make_beam's reduce alone (outside the timed region): the RCCL all-reduce
+        # of the (n_psi + 1) vector, timed over 20 calls on a scratch copy
+        scratch = d_dP.clone()
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+        t_r = time.perf_counter()
+        for _ in range(20):
+            allreduce_deposition(scratch)
+        torch.cuda.synchronize(dev)
+        reduce_ms = (time.perf_counter() - t_r) / 20 * 1e3
+        mine = torch.tensor([kern_ms, post_ms, hot_ms, elapsed / args.steps * 1e3, float(n),
+                             float(ray_steps_local), reduce_ms], dtype=torch.float64, device=dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [a.cpu().numpy() for a in allr]
+        per_rank = {"trace_ms": [float(r[0]) for r in rows], "deposition_ms": [float(r[1]) for r in rows],
+                    "call_ms": [float(r[2]) for r in rows], "step_ms": [float(r[3]) for r in rows],
+                    "rays": [int(r[4]) for r in rows], "ray_steps": [int(r[5]) for r in rows],
+                    "rccl_allreduce_ms": [float(r[6]) for r in rows]}
         dist.all_reduce(tot_steps)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
@@ -369,16 +394,38 @@ def main():
                  "harmonic_integrals_negligible": int(cnt[6]),
                  "harmonic_integrals_settled_early": int(cnt[7])}),
         }
+        if per_rank is not None:
+            out["multi_gpu"] = multi_gpu_block(per_rank, path="torchrun: one process per GPU, "
+                                               "torj_trace_device_ex per rank + torch.distributed "
+                                               "all_reduce of dP_shell")
+        if world == 1 and not args.no_host_api:
+            # the same beam through make_beam's library path (torj_trace_beam_device,
+            # what `--gpus N` in one process times), so an N = 1 point of either path
+            # compares with the N >= 2 lines of both
+            out["library_path"] = library_path_rate(T, plasma, cfg, args, n, d_x0, d_N0, d_w, d_grid,
+                                                    d_xl, d_s0, d_state, d_status, d_steps, d_dP,
+                                                    d_Pdep, d_traj if n_save else None,
+                                                    ray_steps_local, value)
+            progress("library-path steps done")
         if world == 1 and not args.no_host_api:
             out["host_api"] = host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps_local,
                                             pos, s0)
             progress("host-pointer call done")
+            if not args.no_beam_host and args.absorption == "albajar" and not adaptive:
+                out["host_api_beam_c4"] = host_beam_c4(T, plasma, cfg, args, omega, n_save)
+                progress("C4-scale torj_trace_beam call done")
             out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
         if world == 1 and not args.no_cpu_baseline:
             gpu_out = (d_state.cpu().numpy().T, status, d_steps.cpu().numpy())
             out["cpu_baseline"], parity = cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out)
             if parity is not None:
                 out["parity"] = parity
+        elif world > 1 and args.parity_rays > 0 and args.integrator == "rk4":
+            # rank 0's shard against the oracle (bounded sample, untimed)
+            gpu_out = (d_state.cpu().numpy().T, status, d_steps.cpu().numpy())
+            out["parity"] = parity_sample(eq, xp, Np, w, omega, args, grid, gpu_out, args.parity_rays)
+            out["parity"]["shard"] = "rank 0"
+        check_line(out)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -484,19 +531,22 @@ def main_library(args):
         progress(f"warmup {k + 1}/{args.warmup} done")
     sync()
     L = T.lib()
-    T._lib.check(L.torj_timing(plasma.handle, 1))  # replica 0 is the handle: device 0's phases
+    T._lib.check(L.torj_timing(plasma.handle, 1))  # the handle and every replica: per-device phases
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     sync()
     elapsed = time.perf_counter() - t0
     progress(f"timed region done: {elapsed:.2f} s")
-    n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
-    T._lib.check(L.torj_timing_read(plasma.handle, ctypes.byref(n_calls), ctypes.byref(t_trace),
-                                    ctypes.byref(t_post)))
+    calls = (ctypes.c_int * N)()
+    t_trace, t_post = (ctypes.c_double * N)(), (ctypes.c_double * N)()
+    t_red = ctypes.c_double()
+    T._lib.check(L.torj_beam_timing_read(plasma.handle, N, calls, t_trace, t_post, ctypes.byref(t_red)))
     T._lib.check(L.torj_timing(plasma.handle, 0))
-    kern_ms = t_trace.value / max(n_calls.value, 1)
-    post_ms = t_post.value / max(n_calls.value, 1)
+    trace_ms = [t_trace[k] / max(calls[k], 1) for k in range(N)]
+    dep_ms = [t_post[k] / max(calls[k], 1) for k in range(N)]
+    kern_ms, post_ms = trace_ms[0], dep_ms[0]
+    rccl_ms = t_red.value / max(args.steps, 1)
     # the fan-out + reduce overhead alone: empty shards, the same deposition vectors
     empty = [dict(n=0, psi_grid=sh["psi_grid"], dP_shell=sh["dP_shell"]) for sh in shards]
     t1 = time.perf_counter()
@@ -565,8 +615,136 @@ def main_library(args):
             "dP_shell_max_diff_between_devices": agree,
             "deposited_power_sum": float(dP0[-1]),
         },
+        "multi_gpu": multi_gpu_block(
+            {"trace_ms": trace_ms, "deposition_ms": dep_ms, "call_ms": [ms_per_step] * N,
+             "step_ms": [ms_per_step] * N, "rays": [sh["n"] for sh in shards],
+             "ray_steps": [int(c[0]) for c in cnt], "rccl_allreduce_ms": [rccl_ms] * N},
+            path="one process: torj_trace_beam_device, a host thread + stream per device, the "
+                 "library's RCCL all-reduce (ncclCommInitAll)"),
     }
+    if args.parity_rays > 0 and args.integrator == "rk4":
+        sh0 = shards[0]
+        p0 = parts[0]
+        xp0, Np0, _, _ = T.ray_entry(plasma, p0[0], p0[1], omega, args.mode, gpu=True)
+        gpu_out = (sh0["state"].cpu().numpy().T, sh0["status"].cpu().numpy(), sh0["steps"].cpu().numpy())
+        out["parity"] = parity_sample(eq, xp0, Np0, p0[2], omega, args, grid, gpu_out, args.parity_rays)
+        out["parity"]["shard"] = "device 0"
+    check_line(out)
     print(json.dumps(out), flush=True)
+
+
+# keys every bench line carries (the driver's contract), and those of an N >= 2
+# line's multi_gpu block; tests/test_bench_cli.py pins both
+LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+             "scaling", "vs_baseline", "dtype", "data", "config", "roofline")
+MULTI_GPU_KEYS = ("path", "trace_ms_per_device", "deposition_ms_per_device", "call_ms_per_device",
+                  "rays_per_device", "ray_steps_per_device", "trace_ms_max", "trace_ms_min",
+                  "imbalance", "rccl_allreduce_ms")
+
+
+def multi_gpu_block(per, path):
+    """The N >= 2 line's per-device figures: every device's trace-phase and
+    deposition milliseconds (library HIP events), its call time, rays and
+    ray-steps, the spread of the trace phase (max / min - 1) and the RCCL
+    all-reduce of make_beam's reduce (src/solve.jl:233-240)."""
+    tr = [float(v) for v in per["trace_ms"]]
+    return {"path": path,
+            "trace_ms_per_device": tr,
+            "deposition_ms_per_device": [float(v) for v in per["deposition_ms"]],
+            "call_ms_per_device": [float(v) for v in per["call_ms"]],
+            "rays_per_device": [int(v) for v in per["rays"]],
+            "ray_steps_per_device": [int(v) for v in per["ray_steps"]],
+            "trace_ms_max": max(tr), "trace_ms_min": min(tr),
+            "imbalance": max(tr) / max(min(tr), 1e-9) - 1.0,
+            "rccl_allreduce_ms": float(max(per["rccl_allreduce_ms"]))}
+
+
+def check_line(out):
+    """The line's schema (raises before printing a malformed line)."""
+    missing = [k for k in LINE_KEYS if k not in out]
+    if missing:
+        raise KeyError(f"bench line lacks {missing}")
+    if out["n_gpus"] > 1:
+        mg = out.get("multi_gpu")
+        if mg is None or any(k not in mg for k in MULTI_GPU_KEYS):
+            raise KeyError("an N >= 2 line needs the multi_gpu block with " + ", ".join(MULTI_GPU_KEYS))
+        if len(mg["trace_ms_per_device"]) != out["n_gpus"]:
+            raise ValueError("multi_gpu: one trace_ms entry per device")
+    return out
+
+
+def library_path_rate(T, plasma, cfg, args, n, d_x0, d_N0, d_w, d_grid, d_xl, d_s0, d_state, d_status,
+                      d_steps, d_dP, d_Pdep, d_traj, ray_steps, value_main):
+    """The N = 1 beam through torj_trace_beam_device (the library's make_beam
+    fan-out, what `bench.py --gpus N` times in one process) on the same device
+    buffers: min(steps, 10) timed calls after one warm one, host clock with the
+    device drained on both sides, as the headline's timed region."""
+    import torch
+    from torj_hip.parallel import trace_beam_device
+
+    sh = dict(n=n, x0=d_x0, N0=d_N0, weights=d_w, psi_grid=d_grid, x_launch=d_xl, s0=d_s0,
+              state=d_state, status=d_status, steps=d_steps, dP_shell=d_dP, P_dep=d_Pdep, traj=d_traj)
+
+    def call():
+        d_dP.zero_()
+        torch.cuda.synchronize()
+        trace_beam_device(plasma, cfg, args.n_psi, [sh])
+
+    call()
+    k = max(1, min(args.steps, 10))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(k):
+        call()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / k
+    v = ray_steps / dt
+    return {"value": v, "unit": "ray-steps/s", "ms_per_step": dt * 1e3, "steps": k,
+            "vs_headline": v / value_main,
+            "note": "torj_trace_beam_device with one shard on this device (includes the per-call "
+                    "zeroing of dP_shell and the library's synchronous return)"}
+
+
+def host_beam_c4(T, plasma, cfg, args, omega, n_save):
+    """make_beam's host-pointer form (torj_trace_beam, what the Julia shim's
+    make_beam calls) at C4 scale on this device: the 1 005 293-ray fan
+    (N_rings = 291) from pageable host arrays to pageable host arrays, the
+    automatic shards (pinned staging, transfers overlapping the traces), one
+    warm call then one timed.  PCIe-inclusive; reported beside the headline."""
+    from torj_hip import synthetic as S
+
+    setup = S.SETUP
+    N0 = T.pol_tor_angles_2_vector(setup["steering_angle_pol"], setup["steering_angle_tor"])
+    pos, dirs, w = T.launch_peripheral_rays(np.array([setup["R0"], 0.0, setup["z0"]]), N0,
+                                            setup["spot_size"], setup["inverse_curvature_radius"],
+                                            args.freq, N_rings=291, min_azimuthal_points=args.min_az)
+    xp, Np, s0, st = T.ray_entry(plasma, pos, dirs, omega, args.mode, gpu=True)
+    n = len(w)
+    xs, Ns, xl = (np.ascontiguousarray(a.T) for a in (xp, Np, pos))
+    grid = np.linspace(0.0, 1.0, args.n_psi)
+    state, status, steps = np.zeros((7, n)), np.zeros(n, np.int32), np.zeros(n, np.int32)
+    dP, Pdep = np.zeros(args.n_psi + 1), np.zeros(n)
+    traj = np.zeros((max(n_save, 1), 5, n))
+    dp, ip = T._lib.dptr, T._lib.iptr
+    L = T.lib()
+
+    def call():
+        T._lib.check(L.torj_trace_beam(plasma.handle, cfg, n, dp(xs), dp(Ns), dp(w), args.n_psi, dp(grid),
+                                       dp(xl), dp(s0), dp(state), ip(status), ip(steps), dp(dP), dp(Pdep),
+                                       dp(traj) if n_save else None, 1, 0))
+
+    call()
+    t0 = time.perf_counter()
+    call()
+    dt = time.perf_counter() - t0
+    ray_steps = float(steps.sum())
+    return {"value": ray_steps / dt, "unit": "ray-steps/s", "ms": dt * 1e3, "rays": n,
+            "ray_steps": int(ray_steps), "shards": -(-n // 131072),
+            "status_ok": int((status == 0).sum()),
+            "d2h_bytes": int(state.nbytes + status.nbytes + steps.nbytes + Pdep.nbytes
+                             + (traj.nbytes if n_save else 0)),
+            "note": "torj_trace_beam, 1 device, n_shards = 0 (automatic), host arrays both ways "
+                    "incl. PCIe (not the headline)"}
 
 
 def host_api_rate(T, plasma, cfg, xp, Np, w, grid, n_save, ray_steps, pos, s0):
@@ -672,6 +850,95 @@ def pipeline_kernel_ms(stats_csv, kernels):
     return {k: v / launches for k, v in tot.items()}
 
 
+def _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads):
+    """GPU endpoints of the sampled rays (gpu_out: state, status, steps of the
+    whole beam) against the oracle's run r on the same rays."""
+    model = ABSORPTION[args.absorption]
+    warm = model >= 2
+    gs, gst, gk = (a[idx] for a in gpu_out)
+    os_ = r["state"]
+    ex = np.abs(gs[:, :3] - os_[:, :3]).max(1) / np.linalg.norm(os_[:, :3], axis=1)
+    eN = np.abs(gs[:, 3:6] - os_[:, 3:6]).max(1) / np.linalg.norm(os_[:, 3:6], axis=1)
+    # tau relative, floored at 1e-6 (tests/test_gpu_parity.py TAU_FLOOR): below
+    # it the bar is 1e-16 absolute
+    et = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-6)
+    et_strict = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-300)
+    parity = {"rays": int(len(idx)), "vs": "oracle/torj_oracle.c (same RK4, same rays)",
+              "status_equal": bool(np.array_equal(gst, r["status"])),
+              "steps_equal": bool(np.array_equal(gk, r["steps"])),
+              "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
+              "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
+              "max_rel_tau_unfloored": float(et_strict.max()),
+              "max_rel": float(max(ex.max(), eN.max(), et.max())),
+              "rays_within_bar": int((np.maximum(np.maximum(ex, eN), et)
+                                      <= {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)).sum()),
+              "p99_rel_tau": float(np.quantile(et, 0.99)),
+              "worst_tau_ray": {"fan_index": int(idx[int(et.argmax())]),
+                                "tau_gpu": float(gs[int(et.argmax()), 6]),
+                                "tau_cpu": float(os_[int(et.argmax()), 6])},
+              "bar_rel": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10),
+              "bar": (f"x, N: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} relative to "
+                      f"|x|, |N|; tau: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} "
+                      f"relative, i.e. {1e-6 * {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10):g} "
+                      f"absolute below tau = 1e-6 (the floor: P moves by < 1 ulp there); status "
+                      f"and steps exact")}
+    if warm:
+        # a-priori conditioning flag (DESIGN.md 3.6): how far each sampled ray's tau
+        # moves when every RK4 stage point's warm-alpha inputs move by 2^-45 relative
+        # (oracle or_warm_sensitivity, untimed, from the trajectory alone --
+        # independent of the GPU's answer); flagged when that exceeds half the bar
+        bar = {2: 1e-8, 3: 1e-9}[model]
+        t0 = time.perf_counter()
+        sens = OP.warm_sensitivity(xp[idx], Np[idx], omega, args.mode, args.ds, r["steps"],
+                                   iwarm=1 if model == 2 else 3, eta=WARM_FLAG_ETA,
+                                   n_threads=threads)
+        t_sens = time.perf_counter() - t0
+        rel_sens = sens / np.maximum(np.abs(os_[:, 6]), 1e-6)
+        flagged = rel_sens > 0.5 * bar
+        ok = ~flagged
+        e_all = np.maximum(np.maximum(ex, eN), et)
+        parity["conditioning"] = {
+            "flag": "tau sensitivity to 2^-45 relative (128-ulp; at least the GPU Weideman "
+                    "Faddeeva's own 2.5e-14) perturbations of every stage point's alpha inputs "
+                    "(Y up / down, X N_par Te jointly) > bar / 2 (relative, tau floor 1e-6); "
+                    "oracle or_warm_sensitivity, a-priori",
+            "eta": WARM_FLAG_ETA,
+            "rays_flagged": int(flagged.sum()),
+            "rays_unflagged": int(ok.sum()),
+            "rays_within_bar_unflagged": int((e_all[ok] <= bar).sum()),
+            "max_rel_tau_unflagged": float(et[ok].max()) if ok.any() else None,
+            "p99_rel_tau_unflagged": float(np.quantile(et[ok], 0.99)) if ok.any() else None,
+            "rays_out_of_bar_flagged": int((e_all[flagged] > bar).sum()),
+            # the headline figure: every sampled ray, flagged or not
+            "rays_within_bar_all": int((e_all <= bar).sum()),
+            "rays_sampled": int(len(idx)),
+            "seconds": t_sens,
+            "flagged_fan_indices": [int(i) for i in idx[flagged][:64]],
+        }
+        parity["note"] = ("warm model: flagged rays have an optical depth that no double-"
+                          "precision restatement determines to the bar (cold-edge harmonic "
+                          "crossings: fsup's recurrence cancels, and warmdisp's root selector "
+                          "is decided at the 1e-11 level, one ulp of Y picking the other root; "
+                          "50-digit evidence in profiles/r03/c5_conditioning_evidence.json)")
+    return parity
+
+
+def parity_sample(eq, xp, Np, w, omega, args, grid, gpu_out, n_rays):
+    """The oracle on n_rays rays evenly spaced over this beam (untimed): the
+    N >= 2 lines' parity object, as the N = 1 line's cpu_baseline sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+    from torj_hip import synthetic as S
+
+    OP = O.OraclePlasma(*S.plasma_args(eq))
+    O.abs_al_init(24)
+    threads = O.default_threads()
+    idx = np.linspace(0, len(w) - 1, num=min(n_rays, len(w)), dtype=int)
+    r = OP.trace(xp[idx], Np[idx], omega, args.mode, args.ds, args.n_steps, weights=w[idx],
+                 psi_grid=grid, absorption=ABSORPTION[args.absorption], n_threads=threads)
+    return _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads)
+
+
 def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
     """The CPU oracle (C restatement, OpenMP on every host core) on a bounded
     sample of the same rays, warm models included (oracle/torj_warm_oracle.c).
@@ -704,71 +971,7 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
     steps = int(r["steps"].sum())
     parity = None
     if n_steps == args.n_steps and args.integrator == "rk4":
-        gs, gst, gk = (a[idx] for a in gpu_out)
-        os_ = r["state"]
-        ex = np.abs(gs[:, :3] - os_[:, :3]).max(1) / np.linalg.norm(os_[:, :3], axis=1)
-        eN = np.abs(gs[:, 3:6] - os_[:, 3:6]).max(1) / np.linalg.norm(os_[:, 3:6], axis=1)
-        # tau relative, floored at 1e-6 (tests/test_gpu_parity.py TAU_FLOOR): below
-        # it the bar is 1e-16 absolute
-        et = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-6)
-        et_strict = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-300)
-        parity = {"rays": int(len(idx)), "vs": "oracle/torj_oracle.c (same RK4, same rays)",
-                  "status_equal": bool(np.array_equal(gst, r["status"])),
-                  "steps_equal": bool(np.array_equal(gk, r["steps"])),
-                  "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
-                  "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
-                  "max_rel_tau_unfloored": float(et_strict.max()),
-                  "max_rel": float(max(ex.max(), eN.max(), et.max())),
-                  "rays_within_bar": int((np.maximum(np.maximum(ex, eN), et)
-                                          <= {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)).sum()),
-                  "p99_rel_tau": float(np.quantile(et, 0.99)),
-                  "worst_tau_ray": {"fan_index": int(idx[int(et.argmax())]),
-                                    "tau_gpu": float(gs[int(et.argmax()), 6]),
-                                    "tau_cpu": float(os_[int(et.argmax()), 6])},
-                  "bar_rel": {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10),
-                  "bar": (f"x, N: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} relative to "
-                          f"|x|, |N|; tau: {dict({1: 1e-10, 2: 1e-8, 3: 1e-9}).get(model, 1e-10):g} "
-                          f"relative, i.e. {1e-6 * {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10):g} "
-                          f"absolute below tau = 1e-6 (the floor: P moves by < 1 ulp there); status "
-                          f"and steps exact")}
-        if warm:
-            # a-priori conditioning flag: how far each sampled ray's tau
-            # moves when every RK4 stage point's warm-alpha inputs move by 2^-45 relative
-            # (oracle or_warm_sensitivity, untimed, from the trajectory alone --
-            # independent of the GPU's answer); flagged when that exceeds half the bar
-            bar = {2: 1e-8, 3: 1e-9}[model]
-            t0 = time.perf_counter()
-            sens = OP.warm_sensitivity(xp[idx], Np[idx], omega, args.mode, args.ds, r["steps"],
-                                       iwarm=1 if model == 2 else 3, eta=WARM_FLAG_ETA,
-                                       n_threads=threads)
-            t_sens = time.perf_counter() - t0
-            rel_sens = sens / np.maximum(np.abs(os_[:, 6]), 1e-6)
-            flagged = rel_sens > 0.5 * bar
-            ok = ~flagged
-            e_all = np.maximum(np.maximum(ex, eN), et)
-            parity["conditioning"] = {
-                "flag": "tau sensitivity to 2^-45 relative (128-ulp; at least the GPU Weideman "
-                        "Faddeeva's own 2.5e-14) perturbations of every stage point's alpha inputs "
-                        "(Y up / down, X N_par Te jointly) > bar / 2 (relative, tau floor 1e-6); "
-                        "oracle or_warm_sensitivity, a-priori",
-                "eta": WARM_FLAG_ETA,
-                "rays_flagged": int(flagged.sum()),
-                "rays_unflagged": int(ok.sum()),
-                "rays_within_bar_unflagged": int((e_all[ok] <= bar).sum()),
-                "max_rel_tau_unflagged": float(et[ok].max()) if ok.any() else None,
-                "p99_rel_tau_unflagged": float(np.quantile(et[ok], 0.99)) if ok.any() else None,
-                "rays_out_of_bar_flagged": int((e_all[flagged] > bar).sum()),
-                # the headline figure: every sampled ray, flagged or not
-                "rays_within_bar_all": int((e_all <= bar).sum()),
-                "rays_sampled": int(len(idx)),
-                "seconds": t_sens,
-                "flagged_fan_indices": [int(i) for i in idx[flagged][:64]],
-            }
-            parity["note"] = ("warm model: flagged rays have an optical depth that no double-"
-                              "precision restatement determines to the bar (cold-edge harmonic "
-                              "crossings: fsup's recurrence cancels, and warmdisp's root selector "
-                              "is decided at the 1e-11 level, one ulp of Y picking the other root; "
-                              "50-digit evidence in profiles/r03/c5_conditioning_evidence.json)")
+        parity = _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads)
     what = ("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
             else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",

@@ -34,8 +34,9 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 5  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
-                               5: torj_trace_beam_device, torj_power_deposition_profile */
+#define TORJ_ABI_VERSION 6  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
+                               5: torj_trace_beam_device, torj_power_deposition_profile;
+                               6: torj_beam_timing_read, torj_trace_beam's automatic shards */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -237,11 +238,14 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
 /* make_beam's fan-out and reduce across the GPUs of this process
  * (src/solve.jl:209-240: one task per ray, then sum_i w_i dP_dV_i and
  * sum_i w_i P_i).  Host pointers, the arguments and outputs of torj_trace_ex.
- * The rays are cut into n_shards contiguous shards (0: one per GPU; at least
- * n_gpus), their boundaries on 64-ray multiples, dealt round-robin to n_gpus
- * devices: device (p's device + k) mod the device count for k < n_gpus, each
- * with its own copy of the plasma, stream and host thread.  A device runs its
- * shards in turn (upload, trace, deposition, download, torj_trace_check), its
+ * The rays are cut into n_shards contiguous shards (0: automatic -- each
+ * device's share in pieces of at most 131 072 rays, at least one per device;
+ * otherwise at least n_gpus), their boundaries on 64-ray multiples, dealt
+ * round-robin to n_gpus devices: device (p's device + k) mod the device count
+ * for k < n_gpus, each with its own copy of the plasma, stream and host thread.
+ * A device runs its shards in turn through pinned staging in two slots on a
+ * copy stream: shard j + 1's upload and shard j - 1's download overlap shard
+ * j's trace (one torj_trace_check after the last), its
  * dP_shell partial accumulating on the device; the partials are summed over
  * the devices by one RCCL all-reduce of n_psi + 1 fp64 (single-process
  * communicator from ncclCommInitAll, kept on the handle; n_gpus = 1 needs no
@@ -327,6 +331,15 @@ int torj_trace_check(torj_plasma_t p, void *stream);
  * processing milliseconds, then clears. */
 int torj_timing(torj_plasma_t p, int enable);
 int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post_ms);
+
+/* The same per replica of a torj_trace_beam[_device] fan-out (torj_timing(p, 1)
+ * enables it on the handle and every replica): calls, trace_ms, post_ms are
+ * arrays of n_gpus entries (replica k = device (p's device + k) mod count; k = 0
+ * is p), each as torj_timing_read returns it, and reduce_ms the summed host-
+ * clock time of make_beam's RCCL all-reduce (the grouped ncclAllReduce and its
+ * stream waits).  Clears what it reads. */
+int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace_ms, double *post_ms,
+                          double *reduce_ms);
 
 /* power_deposition_profile(plasma, s, x, dP_ds, psi_dP_dV) (src/plasma.jl:91-151)
  * on the GPU for n_rays rays at once: ray r has n_points[r] >= 4 points with

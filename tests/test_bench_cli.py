@@ -33,3 +33,48 @@ def test_world_size_must_match_gpus():
 def test_gpus_below_one_rejected():
     r = _run(["--gpus", "0"])
     assert r.returncode != 0 and "--gpus 0" in r.stderr
+
+
+def _bench_module():
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_under_test", os.path.join(ROOT, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)  # definitions only (main() is behind __name__)
+    return m
+
+
+def _line(n_gpus, **extra):
+    out = {k: None for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step",
+                             "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                             "roofline")}
+    out["n_gpus"] = n_gpus
+    out.update(extra)
+    return out
+
+
+def test_multi_gpu_line_schema():
+    """The N >= 2 line (both launch paths): every device's trace / deposition /
+    call milliseconds, rays and ray-steps, the spread, and the RCCL all-reduce;
+    check_line refuses a line without them, or with a per-device list of the
+    wrong length."""
+    import pytest
+
+    B = _bench_module()
+    per = {"trace_ms": [50.0, 52.0], "deposition_ms": [1.0, 1.1], "call_ms": [55.0, 56.0],
+           "step_ms": [56.0, 56.0], "rays": [100203, 100203], "ray_steps": [200406000, 200406000],
+           "rccl_allreduce_ms": [0.05, 0.06]}
+    mg = B.multi_gpu_block(per, path="test")
+    assert set(B.MULTI_GPU_KEYS) <= set(mg)
+    assert mg["trace_ms_max"] == 52.0 and mg["trace_ms_min"] == 50.0
+    assert abs(mg["imbalance"] - 0.04) < 1e-12 and mg["rccl_allreduce_ms"] == 0.06
+    B.check_line(_line(2, multi_gpu=mg))
+    B.check_line(_line(1))  # N = 1 needs no multi_gpu block
+    with pytest.raises(KeyError):
+        B.check_line(_line(2))
+    with pytest.raises(ValueError):
+        B.check_line(_line(3, multi_gpu=mg))
+    bad = _line(2, multi_gpu=mg)
+    del bad["roofline"]
+    with pytest.raises(KeyError):
+        B.check_line(bad)

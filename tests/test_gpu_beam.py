@@ -195,8 +195,19 @@ def test_trace_beam_device_shards_threaded(gpu, T, hplasma):
         a = T.trace(hplasma, xp, Np, om, 1, **kw)
         cuts = [group_shard(n, 3, k) for k in range(3)]
         sh = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0, cuts, dev)
+        L = T.lib()
+        T._lib.check(L.torj_timing(hplasma.handle, 1))
         with _env(TORJ_BEAM_SAME_DEVICE="1"):
             trace_beam_device(hplasma, cfg, len(grid), sh)
+        # torj_beam_timing_read: one recorded call per replica, a trace phase
+        # each, and no reduce time (the same-device placement sums on the host)
+        import ctypes as C
+        calls, t_tr, t_po, t_red = (C.c_int * 3)(), (C.c_double * 3)(), (C.c_double * 3)(), C.c_double(-1)
+        T._lib.check(L.torj_beam_timing_read(hplasma.handle, 3, calls, t_tr, t_po, C.byref(t_red)))
+        T._lib.check(L.torj_timing(hplasma.handle, 0))
+        assert list(calls) == [1, 1, 1] and all(t > 0 for t in t_tr) and all(t > 0 for t in t_po)
+        assert t_red.value >= 0.0
+        assert L.torj_beam_timing_read(hplasma.handle, 9, calls, t_tr, t_po, None) != 0  # 3 replicas
         c1 = torch.zeros(8, dtype=torch.int64, device=dev)
         one = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0, [slice(0, n)], dev)
         one[0]["counters"] = c1

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -1106,7 +1107,7 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
     if constexpr (MODE == kTrajTile) {
         // one wave per workgroup: the wave's live rays' (R, Z) box, widened by
         // the path the block can take, and its nodes staged in LDS
-        __shared__ double s_tile[kTileNodes * kTileNS];
+        __shared__ __attribute__((aligned(16))) double s_tile[kTileNodes * kTileNS];
         const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
         const double inf = __builtin_inf();
         const double rmin = wave_min(live ? R : inf), rmax = wave_max(live ? R : -inf);
@@ -1132,7 +1133,7 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         if (!live) return;
         traj_run<DEPO, TRAJ, kTileNS>(a, sp, tc, i, x, N, steps, st);
     } else if constexpr (MODE == kTrajLds) {
-        extern __shared__ double s_coef[];
+        extern __shared__ __attribute__((aligned(16))) double s_coef[];
         const int nodes = (a.g.nR + 2) * (a.g.nZ + 2);
         for (int k = threadIdx.x; k < nodes * kTrajLdsNS; k += blockDim.x)
             s_coef[k] = a.coef[(size_t)(k / kTrajLdsNS) * kNF + k % kTrajLdsNS];
@@ -1836,6 +1837,19 @@ struct torj_plasma_s {
     // single-process RCCL communicator over the first nccl_n of them
     std::vector<torj_plasma_s *> replicas;
     std::vector<ncclComm_t> comms;
+    // torj_trace_beam's host staging on this replica (beam_worker): two shard
+    // slots of device buffers and of pinned host buffers (grow-only), the copy
+    // stream and the slots' events (upload done, trace done, download done)
+    struct BeamStage {
+        void *d = nullptr, *h = nullptr;
+        size_t d_cap = 0, h_cap = 0;
+        hipStream_t sc = nullptr;
+        hipEvent_t up[2] = {}, tr[2] = {}, dn[2] = {};
+    } stage;
+    // torj_timing of the all-reduce of make_beam's reduce (beam_reduce, host
+    // clock around the grouped all-reduce and its stream waits)
+    double reduce_ms = 0.0;
+    int reduce_calls = 0;
     // split RK4 path: workspace, the second stream of the
     // alpha / scan kernels and the pipeline's events
     void *d_split = nullptr;
@@ -1936,7 +1950,6 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
         HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
         HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
-        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, lo));
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
             HIPCK(hipEventCreateWithFlags(&p->ev_A[q], hipEventDisableTiming));
@@ -2176,6 +2189,15 @@ int torj_plasma_destroy(torj_plasma_t p) {
     for (ncclComm_t c : p->comms) (void)ncclCommDestroy(c);
     for (size_t k = 1; k < p->replicas.size(); k++) torj_plasma_destroy(p->replicas[k]);
     if (p->d_coef) (void)hipSetDevice(p->device);
+    if (p->stage.sc) (void)hipStreamSynchronize(p->stage.sc);
+    if (p->stage.d) (void)hipFree(p->stage.d);
+    if (p->stage.h) (void)hipHostFree(p->stage.h);
+    for (int r = 0; r < 2; r++) {
+        if (p->stage.up[r]) (void)hipEventDestroy(p->stage.up[r]);
+        if (p->stage.tr[r]) (void)hipEventDestroy(p->stage.tr[r]);
+        if (p->stage.dn[r]) (void)hipEventDestroy(p->stage.dn[r]);
+    }
+    if (p->stage.sc) (void)hipStreamDestroy(p->stage.sc);
     if (p->d_coef) (void)hipFree(p->d_coef);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
@@ -2637,6 +2659,11 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
     hipStream_t s3 = serial ? s : (scan_own ? p->streamS : p->stream2);
     const bool depo_own = dstream && dstream_env == 2 && !serial;
+    if (depo_own && !p->streamD) {  // created on first use only: one more queue otherwise
+        int lo = 0, hi = 0;
+        HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, lo));
+    }
     hipStream_t sD = depo_own ? p->streamD : s3;
     if (!serial) {  // fork from the caller's stream
         HIPCK(hipEventRecord(p->ev_F, s));
@@ -3248,9 +3275,16 @@ int torj_power_deposition_profile(torj_plasma_t p, int n_rays, const int *n_poin
 
 int torj_timing(torj_plasma_t p, int enable) {
     if (!p) return fail("bad plasma handle");
-    p->timing = enable != 0;
-    p->ev_used = 0;
-    p->timing_calls = 0;
+    std::lock_guard<std::mutex> lk(p->mu);
+    // the handle and its torj_trace_beam replicas (new replicas inherit it)
+    for (size_t k = 0; k < std::max<size_t>(1, p->replicas.size()); k++) {
+        torj_plasma_s *q = k == 0 ? p : p->replicas[k];
+        q->timing = enable != 0;
+        q->ev_used = 0;
+        q->timing_calls = 0;
+    }
+    p->reduce_ms = 0.0;
+    p->reduce_calls = 0;
     return 0;
 }
 
@@ -3270,6 +3304,28 @@ int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post
     if (post_ms) *post_ms = q;
     p->ev_used = 0;
     p->timing_calls = 0;
+    return 0;
+}
+
+int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace_ms, double *post_ms,
+                          double *reduce_ms) {
+    if (!p) return fail("bad plasma handle");
+    if (n_gpus < 1) return fail("n_gpus must be >= 1");
+    if (n_gpus > std::max<int>(1, (int)p->replicas.size()))
+        return fail("n_gpus = %d, but the handle has %d replica(s)", n_gpus, std::max<int>(1, (int)p->replicas.size()));
+    int dev0 = 0;
+    HIPCK(hipGetDevice(&dev0));
+    for (int k = 0; k < n_gpus; k++) {
+        torj_plasma_s *q = k == 0 ? p : p->replicas[k];
+        HIPCK(hipSetDevice(q->device));
+        if (torj_timing_read(q, calls ? calls + k : nullptr, trace_ms ? trace_ms + k : nullptr,
+                             post_ms ? post_ms + k : nullptr))
+            return -1;
+    }
+    HIPCK(hipSetDevice(dev0));
+    if (reduce_ms) *reduce_ms = p->reduce_ms;
+    p->reduce_ms = 0.0;
+    p->reduce_calls = 0;
     return 0;
 }
 
@@ -3388,6 +3444,7 @@ static int beam_replicas(torj_plasma_s *p, int n_gpus, bool same) {
         q->vn = p->vn;
         q->vol_coef = p->vol_coef;
         q->psi_prof_max = p->psi_prof_max;
+        q->timing = p->timing;
         p->replicas.push_back(q);
     }
     for (int k = 1; k < n_gpus; k++) {  // scheduling knobs follow the base handle
@@ -3431,8 +3488,20 @@ static int beam_fanout(torj_plasma_s *p, int n_gpus, const char *what, F &&f) {
 // RCCL over xGMI from a single-process communicator (ncclCommInitAll, kept on
 // the handle) enqueued on the replicas' streams; the test-only same-device
 // placement sums on the host.  Synchronous: the replicas' streams are drained.
+static int beam_reduce_run(torj_plasma_s *p, int n_gpus, const std::vector<double *> &d_dP,
+                           int n_psi, bool same);
 static int beam_reduce(torj_plasma_s *p, int n_gpus, const std::vector<double *> &d_dP, int n_psi,
                        bool same) {
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = beam_reduce_run(p, n_gpus, d_dP, n_psi, same);
+    if (p->timing && !rc) {
+        p->reduce_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        p->reduce_calls++;
+    }
+    return rc;
+}
+static int beam_reduce_run(torj_plasma_s *p, int n_gpus, const std::vector<double *> &d_dP,
+                           int n_psi, bool same) {
     const size_t m = (size_t)n_psi + 1;
     if (same) {
         std::vector<double> acc(m, 0.0), part(m);
@@ -3484,8 +3553,48 @@ static void beam_shard(int n, int S, int k, int &lo, int &cnt) {
     cnt = (int)std::min<long>(g1 * 64, n) - lo;
 }
 
-// One device's share: its shards in sequence on the replica's stream, with
-// dP_shell accumulated on the device (d_dP, zeroed here) for the reduce.
+// The staging of torj_trace_beam on replica q: device and pinned host memory
+// for two shard slots of `slot` doubles each, the copy stream and the events.
+static int beam_stage(torj_plasma_s *q, size_t slot) {
+    auto &b = q->stage;
+    if (!b.sc) {
+        HIPCK(hipStreamCreateWithFlags(&b.sc, hipStreamNonBlocking));
+        for (int r = 0; r < 2; r++) {
+            HIPCK(hipEventCreateWithFlags(&b.up[r], hipEventDisableTiming));
+            HIPCK(hipEventCreateWithFlags(&b.tr[r], hipEventDisableTiming));
+            HIPCK(hipEventCreateWithFlags(&b.dn[r], hipEventDisableTiming));
+        }
+    }
+    const size_t bytes = 2 * slot * sizeof(double);
+    if (b.d_cap < bytes) {
+        if (b.d) HIPCK(hipFree(b.d));
+        b.d = nullptr, b.d_cap = 0;
+        HIPCK(hipMalloc(&b.d, bytes));
+        b.d_cap = bytes;
+    }
+    if (b.h_cap < bytes) {
+        if (b.h) HIPCK(hipHostFree(b.h));
+        b.h = nullptr, b.h_cap = 0;
+        HIPCK(hipHostMalloc(&b.h, bytes, hipHostMallocDefault));
+        b.h_cap = bytes;
+    }
+    return 0;
+}
+
+// One device's share of torj_trace_beam: its shards k0, k0 + dk, ... traced on
+// the replica's stream from compact device buffers, with dP_shell accumulated
+// on the device (d_dP, zeroed here) for the reduce.  Host arrays are the
+// caller's (pageable); each shard goes through pinned staging in two slots on
+// a copy stream, pipelined so that shard j + 1's upload and shard j - 1's
+// download overlap shard j's trace:
+//   copy stream  up(0) up(1) [tr 0] dn(0) up(2) [tr 1] dn(1) up(3) ...
+//   trace stream        [up 0] trace(0) [up 1, dn of 2 shards back] trace(1) ...
+// The host packs shard j + 1's inputs into its pinned slot while shard j
+// traces, and unpacks shard j - 2's outputs (waiting for their download)
+// before the slot's next download is queued.  A shard's rows are compact
+// (row r of an array at r * cnt) on both sides, so each transfer is one copy;
+// a slot's input and output blocks sit at fixed offsets (sized for the
+// largest shard), so they never overlap across shards of different sizes.
 static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S, int k0, int dk,
                        const double *x0, const double *N0, const double *w, int n_psi,
                        const double *grid, const double *xl, const double *s0, double *state,
@@ -3493,60 +3602,135 @@ static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S
     if (ensure_device(q)) return -1;
     hipStream_t s = q->stream;
     const bool depo = n_psi >= 2 && grid;
-    const int n_save = cfg->traj_stride > 0 ? cfg->n_steps / cfg->traj_stride : 0;
-    int m = 0;  // largest shard of this device
+    const bool tr_out = traj && cfg->traj_stride > 0 && cfg->n_steps / cfg->traj_stride > 0;
+    const int n_save = tr_out ? cfg->n_steps / cfg->traj_stride : 0;
+    std::vector<int> los, cnts;  // this device's shards
+    int m = 0;
     for (int k = k0; k < S; k += dk) {
         int lo, cnt;
         beam_shard(n, S, k, lo, cnt);
+        if (cnt == 0) continue;
+        los.push_back(lo), cnts.push_back(cnt);
         m = std::max(m, cnt);
     }
     if (depo) HIPCK(hipMemsetAsync(d_dP, 0, (n_psi + 1) * sizeof(double), s));
     if (m == 0) return 0;
     DevBufs B;
-    double *dx0, *dN0, *dw = nullptr, *dgrid = nullptr, *dxl = nullptr, *ds0 = nullptr, *dstate,
-                       *dPdep = nullptr, *dtraj = nullptr;
-    int *dstatus, *dsteps;
-    if (B.alloc(&dx0, 3 * (size_t)m, true) || B.alloc(&dN0, 3 * (size_t)m, true) ||
-        B.alloc(&dstate, 7 * (size_t)m, true) || B.alloc(&dstatus, m, true) || B.alloc(&dsteps, m, true) ||
-        B.alloc(&dw, m, w != nullptr) || B.alloc(&dxl, 3 * (size_t)m, xl != nullptr) ||
-        B.alloc(&ds0, m, s0 != nullptr) || B.alloc(&dPdep, m, depo) ||
-        B.alloc(&dtraj, (size_t)n_save * 5 * m, traj && n_save > 0))
-        return -1;
-    if (depo) {
-        if (B.up(&dgrid, grid, n_psi, s)) return -1;
-    }
+    double *dgrid = nullptr;
+    if (depo && B.up(&dgrid, grid, n_psi, s)) return -1;
+    // rows per shard: inputs x0 N0 [w] [x_launch] [s0]; outputs state [P_dep]
+    // [traj], then status and steps (two int rows in one double row)
+    const int n_in = 6 + (w ? 1 : 0) + (xl ? 3 : 0) + (s0 ? 1 : 0);
+    const int n_out = 7 + (depo ? 1 : 0) + n_save * 5 + 1;
+    const size_t slot = (size_t)(n_in + n_out) * m;
+    if (beam_stage(q, slot)) return -1;
+    auto &bs = q->stage;
+    double *dbase = (double *)bs.d, *hbase = (double *)bs.h;
+    struct View {  // one slot's arrays for a shard of cnt rays
+        double *x0, *N0, *w, *xl, *s0, *state, *Pdep, *traj;
+        int *status, *steps;
+        double *in, *out;  // the contiguous input / output blocks
+        size_t n_in, n_out;  // their sizes in doubles
+    };
+    auto view = [&](double *base, int r, int cnt) {
+        View v{};
+        double *c = base + (size_t)r * slot;
+        v.in = c;
+        v.x0 = c, c += 3 * (size_t)cnt;
+        v.N0 = c, c += 3 * (size_t)cnt;
+        if (w) v.w = c, c += cnt;
+        if (xl) v.xl = c, c += 3 * (size_t)cnt;
+        if (s0) v.s0 = c, c += cnt;
+        v.n_in = c - v.in;
+        // outputs at a fixed offset (m rays' inputs), so a shard's outputs never
+        // share bytes with the next shards' inputs in the same slot: shard
+        // j - 2's download into the host slot can land while shard j's inputs
+        // are packed there
+        c = v.in + (size_t)n_in * m;
+        v.out = c;
+        v.state = c, c += 7 * (size_t)cnt;
+        if (depo) v.Pdep = c, c += cnt;
+        if (n_save) v.traj = c, c += (size_t)n_save * 5 * cnt;
+        v.status = (int *)c, v.steps = (int *)c + cnt, c += cnt;
+        v.n_out = c - v.out;
+        return v;
+    };
     const size_t D = sizeof(double);
-    // rows x cnt sub-block of a (rows x n) SoA host array <-> compact (rows x cnt) device array
-    auto up = [&](double *d, const double *h, int rows, int lo, int cnt) -> int {
-        if (!d || !h) return 0;
-        HIPCK(hipMemcpy2DAsync(d, cnt * D, h + lo, (size_t)n * D, cnt * D, rows, hipMemcpyHostToDevice, s));
+    // rows x cnt sub-block of a (rows x n) SoA host array <-> compact rows
+    auto pack = [&](double *dst, const double *src, int rows, int lo, int cnt) {
+        if (!src) return;
+#pragma omp parallel for if ((size_t)rows * cnt > (1u << 18)) num_threads(8)
+        for (int r = 0; r < rows; r++) memcpy(dst + (size_t)r * cnt, src + (size_t)r * n + lo, cnt * D);
+    };
+    auto unpack = [&](double *dst, const double *src, int rows, int lo, int cnt) {
+        if (!dst) return;
+#pragma omp parallel for if ((size_t)rows * cnt > (1u << 18)) num_threads(8)
+        for (int r = 0; r < rows; r++) memcpy(dst + (size_t)r * n + lo, src + (size_t)r * cnt, cnt * D);
+    };
+    const int nk = (int)los.size();
+    auto stage_in = [&](int j) -> int {  // pack shard j and queue its upload
+        const int r = j & 1, lo = los[j], cnt = cnts[j];
+        if (j >= 2) HIPCK(hipEventSynchronize(bs.up[r]));  // shard j - 2's upload left the slot
+        const View h = view(hbase, r, cnt), d = view(dbase, r, cnt);
+        pack(h.x0, x0, 3, lo, cnt), pack(h.N0, N0, 3, lo, cnt), pack(h.w, w, 1, lo, cnt);
+        pack(h.xl, xl, 3, lo, cnt), pack(h.s0, s0, 1, lo, cnt);
+        HIPCK(hipMemcpyAsync(d.in, h.in, h.n_in * D, hipMemcpyHostToDevice, bs.sc));
+        HIPCK(hipEventRecord(bs.up[r], bs.sc));
         return 0;
     };
-    auto down = [&](double *h, const double *d, int rows, int lo, int cnt) -> int {
-        if (!d || !h) return 0;
-        HIPCK(hipMemcpy2DAsync(h + lo, (size_t)n * D, d, cnt * D, cnt * D, rows, hipMemcpyDeviceToHost, s));
+    auto finish = [&](int j) -> int {  // wait for shard j's download, unpack it
+        const int r = j & 1, lo = los[j], cnt = cnts[j];
+        HIPCK(hipEventSynchronize(bs.dn[r]));
+        const View h = view(hbase, r, cnt);
+        unpack(state, h.state, 7, lo, cnt);
+        if (depo) unpack(P_dep, h.Pdep, 1, lo, cnt);
+        if (n_save) unpack(traj, h.traj, n_save * 5, lo, cnt);
+        memcpy(status + lo, h.status, cnt * sizeof(int));
+        memcpy(steps + lo, h.steps, cnt * sizeof(int));
         return 0;
     };
-    for (int k = k0; k < S; k += dk) {
-        int lo, cnt;
-        beam_shard(n, S, k, lo, cnt);
-        if (cnt == 0) continue;
-        if (up(dx0, x0, 3, lo, cnt) || up(dN0, N0, 3, lo, cnt) || up(dw, w, 1, lo, cnt) ||
-            up(dxl, xl, 3, lo, cnt) || up(ds0, s0, 1, lo, cnt))
-            return -1;
-        if (torj_trace_device_ex(q, cfg, cnt, dx0, dN0, w ? dw : nullptr, depo ? n_psi : 0, dgrid,
-                                 xl ? dxl : nullptr, s0 ? ds0 : nullptr, dstate, dstatus, dsteps,
-                                 depo ? d_dP : nullptr, dPdep, traj && n_save > 0 ? dtraj : nullptr,
+    // TORJ_BEAM_SYNC=1 (read per call; diagnosis): drain the device after every
+    // queued step, so the pipeline runs in program order
+    const char *sync_e = getenv("TORJ_BEAM_SYNC");
+    const bool dbg_sync = sync_e && atoi(sync_e) != 0;
+    auto dsync = [&]() -> int {
+        if (dbg_sync) HIPCK(hipDeviceSynchronize());
+        return 0;
+    };
+    if (stage_in(0) || dsync()) return -1;
+    for (int j = 0; j < nk; j++) {
+        const int r = j & 1, cnt = cnts[j];
+        if (j + 1 < nk && (stage_in(j + 1) || dsync())) return -1;
+        const View d = view(dbase, r, cnt);
+        HIPCK(hipStreamWaitEvent(s, bs.up[r], 0));
+        if (j >= 2) HIPCK(hipStreamWaitEvent(s, bs.dn[r], 0));  // the slot's previous outputs are out
+        if (torj_trace_device_ex(q, cfg, cnt, d.x0, d.N0, d.w, depo ? n_psi : 0, dgrid, d.xl, d.s0,
+                                 d.state, d.status, d.steps, depo ? d_dP : nullptr, d.Pdep, d.traj,
                                  nullptr, s))
             return -1;
-        if (down(state, dstate, 7, lo, cnt) || down(P_dep, depo ? dPdep : nullptr, 1, lo, cnt) ||
-            down(traj, traj && n_save > 0 ? dtraj : nullptr, n_save * 5, lo, cnt) ||
-            ddownload(status + lo, dstatus, cnt, s) || ddownload(steps + lo, dsteps, cnt, s))
-            return -1;
-        // this shard's queue / grid flags, before the replica's scratch is reused
-        if (torj_trace_check(q, s)) return -1;
+        HIPCK(hipEventRecord(bs.tr[r], s));
+        if (dsync()) return -1;
+        if (j >= 2 && finish(j - 2)) return -1;  // before this slot's host buffer is reused
+        const View h = view(hbase, r, cnt);
+        HIPCK(hipStreamWaitEvent(bs.sc, bs.tr[r], 0));
+        HIPCK(hipMemcpyAsync(h.out, d.out, d.n_out * D, hipMemcpyDeviceToHost, bs.sc));
+        HIPCK(hipEventRecord(bs.dn[r], bs.sc));
     }
-    return 0;
+    for (int j = std::max(0, nk - 2); j < nk; j++)
+        if (finish(j)) return -1;
+    // every shard's queue / grid flags (sticky since the last check)
+    return torj_trace_check(q, s);
+}
+
+// Shards of torj_trace_beam when the caller leaves n_shards = 0: each device's
+// share in pieces of at most kBeamAutoRays rays (at least one per device), so
+// the host transfers of one piece overlap the trace of the next (beam_worker)
+// while every piece still fills the device (the split pipeline wants >= ~1e5
+// rays: a 1e5-ray beam stays one piece).
+constexpr long kBeamAutoRays = 131072;
+static int beam_auto_shards(int n, int n_gpus) {
+    const long per = ((long)n + n_gpus - 1) / n_gpus;
+    return n_gpus * (int)std::max<long>(1, (per + kBeamAutoRays - 1) / kBeamAutoRays);
 }
 
 extern "C" {
@@ -3570,7 +3754,7 @@ int torj_trace_beam(torj_plasma_t p, const torj_trace_cfg *cfg, int n, const dou
     }
     const bool same = beam_same_device();
     if (beam_replicas(p, n_gpus, same)) return -1;
-    const int S = std::max(n_shards > 0 ? n_shards : n_gpus, n_gpus);
+    const int S = n_shards > 0 ? std::max(n_shards, n_gpus) : beam_auto_shards(n, n_gpus);
     const char *rccl_e = getenv("TORJ_BEAM_RCCL");  // read per call (tests toggle it)
     const bool reduce = depo && (n_gpus > 1 || (rccl_e && atoi(rccl_e) != 0));
     // per-device partial dP_shell, then one all-reduce

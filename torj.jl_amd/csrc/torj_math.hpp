@@ -239,6 +239,28 @@ struct FieldPack {
 //   v = sum wZ wR c, gr = sum wZ dwR c, gz = sum dwZ wR c, grz = sum dwZ dwR c
 // The same arithmetic whatever memory c0 points into (global / L2 or an LDS
 // tile), so the results do not depend on where the coefficients were read.
+// 16-byte view of a coefficient pointer, in its address space: the 6-field
+// layouts of the LDS-staged coefficients (48 B per node) are read a field pair
+// at a time (ds_read_b128, 256 B/clk/CU, where two 8-byte reads merge into a
+// ds_read2_b64 at 128 B/clk/CU)
+struct alignas(16) Dbl2 {
+    double x, y;
+};
+template <class P>
+struct Pair16Ptr {
+    using type = const Dbl2 *;
+};
+#ifdef __HIP_DEVICE_COMPILE__
+template <>
+struct Pair16Ptr<const __attribute__((address_space(3))) double *> {
+    using type = const __attribute__((address_space(3))) Dbl2 *;
+};
+template <>
+struct Pair16Ptr<const __attribute__((address_space(1))) double *> {
+    using type = const __attribute__((address_space(1))) Dbl2 *;
+};
+#endif
+
 template <int NGRAD, int NVAL, bool EXT, int NS, class P = const double *>
 TORJ_HD void stencil_sums(P c0, int rs, const Axis &aR, const Axis &aZ,
                           const int (&fidx)[NGRAD + NVAL], double (&v)[NGRAD + NVAL],
@@ -247,6 +269,51 @@ TORJ_HD void stencil_sums(P c0, int rs, const Axis &aR, const Axis &aZ,
     constexpr int NT = NGRAD + NVAL;
 #pragma unroll
     for (int f = 0; f < NT; f++) v[f] = gr[f] = gz[f] = grz[f] = 0.0;
+    // one field's sums, from its 4 coefficients of row b (the order of every
+    // fma is the same whichever way the coefficients were read)
+    auto field = [&](int f, int b, const double (&c)[4]) {
+        const bool slopes = EXT || f < NGRAD;
+        double sv = 0.0, sd = 0.0;
+#pragma unroll
+        for (int a = 0; a < 4; a++) {
+            sv = fma(aR.w[a], c[a], sv);
+            if (slopes) sd = fma(aR.dw[a], c[a], sd);
+        }
+        v[f] = fma(aZ.w[b], sv, v[f]);
+        if (slopes) {
+            gz[f] = fma(aZ.dw[b], sv, gz[f]);
+            gr[f] = fma(aZ.w[b], sd, gr[f]);
+        }
+        if (EXT && f < NGRAD) grz[f] = fma(aZ.dw[b], sd, grz[f]);
+    };
+    if constexpr (NS == 6) {
+        // the 6-field layouts: per row, one field pair of the 4 nodes at a time
+        // (4 x ds_read_b128 for two fields, short live ranges)
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+            const P row = c0 + (size_t)b * rs;
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                bool need = false;
+#pragma unroll
+                for (int f = 0; f < NT; f++) need = need || (fidx[f] >> 1) == k;
+                if (!need) continue;
+                double lo[4], hi[4];
+#pragma unroll
+                for (int a = 0; a < 4; a++) {
+                    const Dbl2 d = reinterpret_cast<typename Pair16Ptr<P>::type>(row + a * NS)[k];
+                    lo[a] = d.x, hi[a] = d.y;
+                }
+#pragma unroll
+                for (int f = 0; f < NT; f++)
+                    if (fidx[f] == 2 * k)
+                        field(f, b, lo);
+                    else if (fidx[f] == 2 * k + 1)
+                        field(f, b, hi);
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int b = 0; b < 4; b++) {
         const P row = c0 + (size_t)b * rs;
@@ -593,17 +660,25 @@ struct GLTable {
     int n;
     int negl_skip;  // 1: skip harmonic integrals provably below an ulp of the sum (default)
     double t[kMaxGL], w[kMaxGL], st[kMaxGL], t2[kMaxGL];  // nodes, weights, sqrt(1-t^2), t^2
-    // the node loop's per-node constants (pair_term): s2 = 1 - t^2 and the
-    // weights with the Bessel argument's node factor folded in, wm[m-2] = w s2^m
-    double s2[kMaxGL], wm[2][kMaxGL];
+    // the node loop's per-node constants (pair_term), per harmonic m, one
+    // 32-byte record per node (one scalar load of 8 dwords per pair): t, t^2,
+    // s2 = 1 - t^2 and the weight with the Bessel argument's node factor folded
+    // in, w s2^m
+    struct Node {
+        double t, t2, s2, wm;
+    } nd[2][kMaxGL];
 };
-// s2 and wm of node i from its t and w (host, at abs_Al_init), in long double
-// so that each folded weight is rounded once
+// the node records of node i from its t and w (host, at abs_Al_init), in long
+// double so that each folded weight is rounded once
 inline void gl_node_consts(GLTable &g, int i) {
     const long double t = g.t[i], s2 = 1.0L - t * t, w = g.w[i];
-    g.s2[i] = (double)s2;
-    g.wm[0][i] = (double)(w * s2 * s2);
-    g.wm[1][i] = (double)(w * s2 * s2 * s2);
+    for (int m = 2; m <= 3; m++) {
+        GLTable::Node &q = g.nd[m - 2][i];
+        q.t = g.t[i];
+        q.t2 = g.t[i] * g.t[i];
+        q.s2 = (double)s2;
+        q.wm = (double)(m == 2 ? w * s2 * s2 : w * s2 * s2 * s2);
+    }
 }
 
 #ifndef TORJ_ALBAJAR_NOINLINE
@@ -728,12 +803,6 @@ struct SeriesCoefs {
 // harmonic (no quotient: K1 and K5 carry a factor x_m = 2 hx), and hx^(2m)
 // applied once to the sum (albajar_harmonic): 25 VALU per pair besides the
 // series, square roots and exponentials, against 34 for the direct form.
-template <int M>
-TORJ_HD double gl_wm(const GLTable &gl, int i) {
-    static_assert(M == 2 || M == 3, "the Albajar sum has harmonics 2 and 3");
-    return gl.wm[M - 2][i];
-}
-
 template <int M, int LV>
 TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, double t, double s2,
                          double W, double t2, bool single) {
@@ -760,6 +829,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     SeriesCoefs<M, LV> sc;
     sc.load();
     const int n = gl.n, half = n >> 1;
+    const GLTable::Node *nd = gl.nd[M - 2];
 #ifdef __HIP_DEVICE_COMPILE__
     if constexpr (LPR > 1) {
         // LPR lanes per ray (small beams, latency-bound): lane `sub` of the ray's
@@ -774,7 +844,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
             rr[q] = 0.0;
             const int i = q * LPR + sub;
             if (q * LPR < half && i < half)
-                rr[q] = pair_term<M, LV>(c, sc, gl.t[i], gl.s2[i], gl_wm<M>(gl, i), gl.t2[i], false);
+                rr[q] = pair_term<M, LV>(c, sc, nd[i].t, nd[i].s2, nd[i].wm, nd[i].t2, false);
         }
         const int base = (int)(threadIdx.x & 63u) & ~(LPR - 1);
         double s = 0.0;
@@ -787,7 +857,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
                 if (q * LPR + u < half) s += v;
             }
         }
-        if (n & 1) s += pair_term<M, LV>(c, sc, gl.t[half], gl.s2[half], gl_wm<M>(gl, half), gl.t2[half], true);
+        if (n & 1) s += pair_term<M, LV>(c, sc, nd[half].t, nd[half].s2, nd[half].wm, nd[half].t2, true);
         return s;
     }
 #endif
@@ -795,48 +865,25 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
 #pragma unroll
     for (int u = 0; u < U; u++) acc[u] = 0.0;
     // U independent node pairs per iteration (ILP for the dependent fp64
-    // chains), with the (uniform, scalar-loaded) node constants of the next U
-    // pairs fetched while these compute (gl arrays hold kMaxGL >= half + U
-    // entries, so the look-ahead never leaves the table)
-    double tn[U], sn[U], wn[U], qn[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        tn[u] = gl.t[u];
-        sn[u] = gl.s2[u];
-        wn[u] = gl_wm<M>(gl, u);
-        qn[u] = gl.t2[u];
-    }
+    // chains); each pair's four constants are one 32-byte record (one scalar
+    // load, uniform across the wave; a look-ahead load of the next record,
+    // consumed at the end of the iteration, is scheduled late by the compiler
+    // anyway, and the other waves of the SIMD cover the latency)
     int i = 0;
 #pragma unroll 1
     for (; i + U <= half; i += U) {
-        double t[U], st[U], w[U], q[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            t[u] = tn[u];
-            st[u] = sn[u];
-            w[u] = wn[u];
-            q[u] = qn[u];
-            tn[u] = gl.t[i + U + u];
-            sn[u] = gl.s2[i + U + u];
-            wn[u] = gl_wm<M>(gl, i + U + u);
-            qn[u] = gl.t2[i + U + u];
-        }
         double r[U];
 #pragma unroll
-        for (int u = 0; u < U; u++) r[u] = pair_term<M, LV>(c, sc, t[u], st[u], w[u], q[u], false);
-#ifdef __HIP_DEVICE_COMPILE__
-        // consume the prefetched constants at the END of the iteration, so the
-        // s_load latency hides behind these pairs (otherwise load PRE re-rolls
-        // them to the loop head, right before their first use)
-#pragma unroll
-        for (int u = 0; u < U; u++) asm volatile("" : "+s"(tn[u]), "+s"(sn[u]), "+s"(wn[u]), "+s"(qn[u]));
-#endif
+        for (int u = 0; u < U; u++) {
+            const GLTable::Node q = nd[i + u];
+            r[u] = pair_term<M, LV>(c, sc, q.t, q.s2, q.wm, q.t2, false);
+        }
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, gl.t[i], gl.s2[i], gl_wm<M>(gl, i), gl.t2[i], false);
-    if (n & 1) acc[0] += pair_term<M, LV>(c, sc, gl.t[half], gl.s2[half], gl_wm<M>(gl, half), gl.t2[half], true);
+    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, nd[i].t, nd[i].s2, nd[i].wm, nd[i].t2, false);
+    if (n & 1) acc[0] += pair_term<M, LV>(c, sc, nd[half].t, nd[half].s2, nd[half].wm, nd[half].t2, true);
     double s = acc[0];
 #pragma unroll
     for (int u = 1; u < U; u++) s += acc[u];

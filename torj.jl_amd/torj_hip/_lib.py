@@ -93,6 +93,7 @@ _SIGS = {
     "torj_trace_check": (C.c_int, [C.c_void_p, C.c_void_p]),
     "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "torj_timing_read": (C.c_int, [C.c_void_p, _ip, _dp, _dp]),
+    "torj_beam_timing_read": (C.c_int, [C.c_void_p, C.c_int, _ip, _dp, _dp, _dp]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -105,7 +106,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 5  # include/torj_hip.h TORJ_ABI_VERSION
+ABI_VERSION = 6  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 
