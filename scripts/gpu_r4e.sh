@@ -6,7 +6,9 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r4e
 mkdir -p $O/profiles
-bash scripts/gpu_ab.sh r4e/b128 nob128 base nob128 base || exit 1
+timeout -k 10 900 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py tests/test_gpu_c3.py -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+bash scripts/gpu_ab.sh r4e/b128 nob128 nomove base nob128 nomove base || exit 1
 for v in base nob128; do
   if [ $v = base ]; then L=$PWD/torj.jl_amd/build/libtorj_hip.so; else L=$PWD/torj.jl_amd/build/variants/libtorj_hip_$v.so; fi
   (cd /tmp && TORJ_HIP_LIB=$L TORJ_SPLIT_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/serial_$v -o s -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-host-api --steps 3 > $GRAFT_REPO_ROOT/$O/serial_$v.log 2>&1) || { echo serial $v failed; tail -5 $O/serial_$v.log; exit 1; }
@@ -29,3 +31,5 @@ for k, v in t.items():
         print(k, len(n[k]), {c: round(x / 1e9, 3) for c, x in v.items()})
 PY
 bash scripts/gpu_ring_ab.sh r4e/ring || exit 1
+TORJ_BENCH_SAME_DEVICE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 3 --warmup 1 > $O/trun2.log 2>&1 || { tail -30 $O/trun2.log; exit 1; }
+grep '^{' $O/trun2.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('trun2', d['value'], d['ms_per_step'], d['multi_gpu']['trace_ms_per_device'])"

@@ -879,7 +879,7 @@ __global__ void __launch_bounds__(64, ABS >= 2 ? TORJ_WARM_MIN_WAVES : TORJ_MIN_
 // group at one (step, stage): the same lanes as the fused kernel's wave there,
 // so the per-wave Bessel-level ballot and every alpha are the same bits.
 // ---------------------------------------------------------------------------
-constexpr int kAinF = 5;  // X, Y, |N|, N_par, Te (+ 1 / |dD/dN| for the warm alpha: kAinFW)
+constexpr int kAinF = 5;  // X, Y, |N|^2, N_par, ln Te (warm: X, Y, |N|, N_par, Te, 1 / |dD/dN|: kAinFW)
 constexpr int kAinFW = 6;
 
 struct SplitArgs {
@@ -939,8 +939,11 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
                 o[4 * (size_t)a.n] = exp(p.lnTe);
                 o[kAinF * (size_t)a.n] = inv;
             } else {
-                o[2 * (size_t)a.n] = sqrt_pos(N2);
-                o[4 * (size_t)a.n] = exp_fast(p.lnTe);
+                // |N|^2 and ln Te: k_alpha_pts takes the square root and the
+                // exponential (the same functions ray_rhs applies), off the
+                // latency-bound trajectory chain and onto the parallel alpha lanes
+                o[2 * (size_t)a.n] = N2;
+                o[4 * (size_t)a.n] = p.lnTe;
             }
         }
         const double wgt = (st == 0 || st == 3) ? 1.0 : 2.0;
@@ -1187,18 +1190,17 @@ __global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a
     // alpha the scan never reads
     if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
     const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
+    const double Nabs = sqrt_pos(in[2 * (size_t)a.n]), Te = exp_fast(in[4 * (size_t)a.n]);
     if constexpr (COUNT) {
         AlbajarWork work = {};
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
-            in[4 * (size_t)a.n], a.mode, &work);
+            c_gl, a.omega, in[0], in[(size_t)a.n], Nabs, in[3 * (size_t)a.n], Te, a.mode, &work);
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
                                      ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
     } else {
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n], in[3 * (size_t)a.n],
-            in[4 * (size_t)a.n], a.mode, nullptr);
+            c_gl, a.omega, in[0], in[(size_t)a.n], Nabs, in[3 * (size_t)a.n], Te, a.mode, nullptr);
     }
 }
 
