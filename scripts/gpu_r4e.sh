@@ -8,7 +8,7 @@ O=gpurun_out/r4e
 mkdir -p $O/profiles
 timeout -k 10 900 python -u -m pytest tests/test_gpu_split.py tests/test_gpu_parity.py tests/test_gpu_c3.py -x -q --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
 tail -1 $O/pytest.log
-bash scripts/gpu_ab.sh r4e/b128 nob128 nomove base nob128 nomove base || exit 1
+bash scripts/gpu_ab.sh r4e/b128 nob128 nomove noscan base nob128 nomove noscan base || exit 1
 for v in base nob128; do
   if [ $v = base ]; then L=$PWD/torj.jl_amd/build/libtorj_hip.so; else L=$PWD/torj.jl_amd/build/variants/libtorj_hip_$v.so; fi
   (cd /tmp && TORJ_HIP_LIB=$L TORJ_SPLIT_SERIAL=1 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/serial_$v -o s -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-host-api --steps 3 > $GRAFT_REPO_ROOT/$O/serial_$v.log 2>&1) || { echo serial $v failed; tail -5 $O/serial_$v.log; exit 1; }

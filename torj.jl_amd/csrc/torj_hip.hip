@@ -1277,68 +1277,88 @@ __device__ __forceinline__ void tau_scan_body(const TraceArgs &a, const SplitArg
             double P = exp(-tau);  // bitwise the value the previous step computed
             DepoAcc dacc = {-1, 0.0};
             const int s_end = min(a.n_steps, sp.k0 + sp.kb);
-            for (int s = steps; s < s_end; s++) {
-                if (s >= tT) {  // the trajectory stopped before step s
-                    if (tS == ST_NAN) st = ST_NAN;  // non-finite x / N at step s (ray_segment's `bad`)
-                    break;
-                }
-                const size_t o = (size_t)(s - sp.k0) * 4 * a.n + i;
-                const double al0 = sp.alpha[o], al1 = sp.alpha[o + a.n], al2 = sp.alpha[o + 2 * (size_t)a.n],
-                             al3 = sp.alpha[o + 3 * (size_t)a.n];
-                double acc_a = fma(1.0, al0, 0.0);
-                acc_a = fma(2.0, al1, acc_a);
-                acc_a = fma(2.0, al2, acc_a);
-                acc_a = fma(1.0, al3, acc_a);
-                const double taun = tau + ds6 * acc_a;
-                if (!isfinite(taun)) {  // alpha went non-finite: NAN at step s, state x_s
-                    st = ST_NAN | 0x40;  // internal: the final state needs the replay
-                    break;
+            // the steps' alphas are loaded kScanBatch steps at a time (one memory
+            // latency per batch instead of one per step: the scan is a serial
+            // chain per lane); the loads stay inside the block's ring slot
+            constexpr int kScanBatch = 4;
+            bool done = false;
+            for (int sb = steps; sb < s_end && !done; sb += kScanBatch) {
+                double alb[kScanBatch][4];
+#pragma unroll
+                for (int v = 0; v < kScanBatch; v++) {
+                    const size_t ov = (size_t)(min(sb + v, s_end - 1) - sp.k0) * 4 * a.n + i;
+#pragma unroll
+                    for (int q = 0; q < 4; q++) alb[v][q] = sp.alpha[ov + q * (size_t)a.n];
                 }
 #pragma unroll
-                for (int q = 0; q < 4 && COUNT; q++) {
-                    const unsigned wk = sp.awork[o + q * (size_t)a.n];
-                    if (am == 1) {
-                        c2 += wk & 1u;
-                        c3 += (wk >> 1) & 3u;
-                        c5 += (wk >> 3) & 3u;
-                        c4 += (wk >> 5) & 2047u;
-                        c6 += (wk >> 16) & 3u;
-                        c7 += (wk >> 18) & 3u;
-                    } else if (am == 2) {
-                        const unsigned lrm = wk >> 21, passes = (wk >> 14) & 127u;
-                        c2 += wk & 127u;
-                        c3 += (wk >> 7) & 127u;
-                        c4 += passes;
-                        c5 += passes * lrm;
-                        c6 += lrm;
-                        c7 += lrm * lrm;
+                for (int v = 0; v < kScanBatch; v++) {
+                    const int s = sb + v;
+                    if (s >= s_end) break;
+                    if (s >= tT) {  // the trajectory stopped before step s
+                        if (tS == ST_NAN) st = ST_NAN;  // non-finite x / N at step s (ray_segment's `bad`)
+                        done = true;
+                        break;
                     }
-                }
-                const double Pn = exp(-taun);
-                const double dP = P - Pn;
-                if constexpr (DEPO == kDepoSamples) {
-                    if (s > 0) a.smp_dpds[smp_at(s, i, a.smp_rows)] = P * al0;
-                }
-                tau = taun;
-                P = Pn;
-                steps = s + 1;
-                nsteps++;
-                if constexpr (DEPO == kDepoBinned) {
-                    const double psi_b = sp.psib[(size_t)(s - sp.k0) * a.n + i];
-                    Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
-                    psi_a = psi_b;
-                }
-                if constexpr (TRAJ) {
-                    if (a.traj_stride > 0 && (steps % a.traj_stride) == 0)
-                        a.traj[((size_t)(steps / a.traj_stride - 1) * 5 + 3) * a.n + i] = tau;
-                }
-                if (steps == tT && tS == ST_LEFT_PLASMA) {  // psi check first (src/solve.jl:174)
-                    st = ST_LEFT_PLASMA;
-                    break;
-                }
-                if (a.chunk_steps > 0 && (steps % a.chunk_steps) == 0 && P < a.P_min) {  // :176
-                    st = ST_ABSORBED;
-                    break;
+                    const size_t o = (size_t)(s - sp.k0) * 4 * a.n + i;
+                    const double al0 = alb[v][0], al1 = alb[v][1], al2 = alb[v][2], al3 = alb[v][3];
+                    double acc_a = fma(1.0, al0, 0.0);
+                    acc_a = fma(2.0, al1, acc_a);
+                    acc_a = fma(2.0, al2, acc_a);
+                    acc_a = fma(1.0, al3, acc_a);
+                    const double taun = tau + ds6 * acc_a;
+                    if (!isfinite(taun)) {  // alpha went non-finite: NAN at step s, state x_s
+                        st = ST_NAN | 0x40;  // internal: the final state needs the replay
+                        done = true;
+                        break;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4 && COUNT; q++) {
+                        const unsigned wk = sp.awork[o + q * (size_t)a.n];
+                        if (am == 1) {
+                            c2 += wk & 1u;
+                            c3 += (wk >> 1) & 3u;
+                            c5 += (wk >> 3) & 3u;
+                            c4 += (wk >> 5) & 2047u;
+                            c6 += (wk >> 16) & 3u;
+                            c7 += (wk >> 18) & 3u;
+                        } else if (am == 2) {
+                            const unsigned lrm = wk >> 21, passes = (wk >> 14) & 127u;
+                            c2 += wk & 127u;
+                            c3 += (wk >> 7) & 127u;
+                            c4 += passes;
+                            c5 += passes * lrm;
+                            c6 += lrm;
+                            c7 += lrm * lrm;
+                        }
+                    }
+                    const double Pn = exp(-taun);
+                    const double dP = P - Pn;
+                    if constexpr (DEPO == kDepoSamples) {
+                        if (s > 0) a.smp_dpds[smp_at(s, i, a.smp_rows)] = P * al0;
+                    }
+                    tau = taun;
+                    P = Pn;
+                    steps = s + 1;
+                    nsteps++;
+                    if constexpr (DEPO == kDepoBinned) {
+                        const double psi_b = sp.psib[(size_t)(s - sp.k0) * a.n + i];
+                        Pdep += deposit(a, dacc, psi_a, psi_b, dP, w);
+                        psi_a = psi_b;
+                    }
+                    if constexpr (TRAJ) {
+                        if (a.traj_stride > 0 && (steps % a.traj_stride) == 0)
+                            a.traj[((size_t)(steps / a.traj_stride - 1) * 5 + 3) * a.n + i] = tau;
+                    }
+                    if (steps == tT && tS == ST_LEFT_PLASMA) {  // psi check first (src/solve.jl:174)
+                        st = ST_LEFT_PLASMA;
+                        done = true;
+                        break;
+                    }
+                    if (a.chunk_steps > 0 && (steps % a.chunk_steps) == 0 && P < a.P_min) {  // :176
+                        st = ST_ABSORBED;
+                        done = true;
+                        break;
+                    }
                 }
             }
             if constexpr (DEPO == kDepoBinned) depo_flush(a, dacc);
