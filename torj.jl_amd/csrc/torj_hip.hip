@@ -2849,13 +2849,19 @@ int torj_trace_device_ex(torj_plasma_t p, const torj_trace_cfg *cfg, int n, cons
     if (n <= 0) return 0;
     if (p->timing) p->timing_calls++;
     const bool fit = n_psi >= 2 && grid && dP && cfg->deposition == 1;
-    if (fit && cfg->n_steps > 0 && x0 && N0 && state && status && steps) {
+    // TORJ_SPLIT_BATCH=R (read per call; fixed-step absorbing beams): trace in
+    // contiguous batches of R rays (a multiple of 64), each its own pipeline
+    const char *sb_e = getenv("TORJ_SPLIT_BATCH");
+    const long sb_rays = (sb_e && cfg->integrator == 0 && cfg->absorption >= 1) ? atol(sb_e) / 64 * 64 : 0;
+    if ((fit || sb_rays > 0) && cfg->n_steps > 0 && x0 && N0 && state && status && steps) {
         const size_t K = (size_t)cfg->n_steps + 2, L = (size_t)n_psi;
-        const size_t per_ray = (cfg->integrator == 1 ? 6 : 5) * 8 * K + 4 * (L + 1) + 16 * L + 4;
+        const size_t per_ray = fit ? (cfg->integrator == 1 ? 6 : 5) * 8 * K + 4 * (L + 1) + 16 * L + 4 : 0;
         if (ensure_device(p)) return -1;
         const size_t budget = ws_budget(p);
-        if ((size_t)n * per_ray > budget) {
-            const int nb = (int)std::max<size_t>(64, budget / per_ray / 64 * 64);
+        size_t nb_ws = fit && (size_t)n * per_ray > budget ? std::max<size_t>(64, budget / per_ray / 64 * 64) : (size_t)n;
+        if (sb_rays > 0 && (size_t)sb_rays < nb_ws) nb_ws = (size_t)sb_rays;
+        if (nb_ws < (size_t)n) {
+            const int nb = (int)nb_ws;
             hipStream_t s = (hipStream_t)stream;
             const int n_save = cfg->traj_stride > 0 && traj ? cfg->n_steps / cfg->traj_stride : 0;
             const size_t D = sizeof(double), B = (size_t)nb;
