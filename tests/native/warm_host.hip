@@ -168,9 +168,18 @@ void fd_profile_stream(int n, int n_steps, int n_psi, double ds, const double *g
     fa.kstar = kstar;
     fa.Pray = Pray;
     for (int i = 0; i < n; i++) {
-        // as k_depo_stream: psi at the launch point only for the walk's start
-        for (int S = inc; S < steps[i]; S += inc)
-            torj::fit_depo_stream(fa, dst, i, dsv[torj::kDsJ * N + i] < 0 ? psiL[i] : 0.0, S);
+        // as k_depo_stream: psi at the launch point only for the walk's start;
+        // inc < 0: the split form (k_depo_elim then k_depo_walk, one window per block)
+        const int step = inc < 0 ? -inc : inc;
+        for (int S = step; S < steps[i]; S += step) {
+            const double pl = dsv[torj::kDsJ * N + i] < 0 ? psiL[i] : 0.0;
+            if (inc < 0) {
+                torj::fit_depo_stream_elim(fa, dst, i, pl, S);
+                torj::fit_depo_stream_walk(fa, dst, i, pl, S);
+            } else {
+                torj::fit_depo_stream(fa, dst, i, pl, S);
+            }
+        }
         torj::fit_depo_tail(fa, dst, i, psiL[i]);
     }
     for (size_t k = 0; k + 1 < L; k++)

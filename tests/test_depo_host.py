@@ -31,8 +31,9 @@ def _d(a):
 
 
 def _run(H, n_steps, grid, s0, steps, psiL, smp, nc, ds=1e-4, stream=0):
-    """nc: the open-shell cache; stream > 0: the streamed walk (fd_profile_stream,
-    the scan's steps growing by `stream` per emulated block)"""
+    """nc: the open-shell cache; stream != 0: the streamed walk (fd_profile_stream,
+    the scan's steps growing by |stream| per emulated block; < 0 the split form,
+    elimination and walk of one window per block)"""
     n = len(s0)
     psi = np.ascontiguousarray(smp[:, :, 0].T)   # (n_steps + 1) x n
     dpds = np.ascontiguousarray(smp[:, :, 1].T)
@@ -88,6 +89,10 @@ def test_host_deposition_matches_fitpack(H, T, hplasma, oplasma, mode, grid_kind
     d60, k60, P60 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], 2, stream=60)
     d37, k37, P37 = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], 2, stream=37)
     assert np.array_equal(k60, k37) and np.array_equal(P60, P37) and np.array_equal(d60, d37)
+    # the split form (TORJ_DEPO_STREAM=3: elimination and walk of one window as
+    # two launches per block): the same windows, the same bits
+    ds_, ks_, Ps_ = _run(H, n_steps, grid, s0, o["steps"], psiL, o["samples"], 2, stream=-60)
+    assert np.array_equal(k60, ks_) and np.array_equal(P60, Ps_) and np.array_equal(d60, ds_)
     assert np.array_equal(k60, kstar)
     assert np.abs(P60 - P).max() <= 1e-13 * P.max()
     assert np.abs(d60 - dPs).max() <= 1e-13 * np.abs(dPs).max()

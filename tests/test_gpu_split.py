@@ -308,7 +308,7 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     out = {}
     old = os.environ.get("TORJ_DEPO_STREAM")
     try:
-        for mode in ("0", "1", "2"):
+        for mode in ("0", "1", "2", "3"):
             os.environ["TORJ_DEPO_STREAM"] = mode
             out[mode] = _run(T, hplasma, 3, 90, xp, Np, om, 1, **kw)
     finally:
@@ -326,9 +326,11 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     assert np.abs(a.dP_shell).max() > 0
     # the windows on a stream of their own (TORJ_DEPO_STREAM=2, overlapping the
     # next block's scan): the same windows, so the same bits as on the scan's stream
-    c = out["2"]
-    for f in ("state", "status", "steps", "P_dep", "dP_shell"):
-        assert np.array_equal(getattr(b, f), getattr(c, f)), f
+    # and the split form (=3: a window's elimination and walk as two launches)
+    for m in ("2", "3"):
+        c = out[m]
+        for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+            assert np.array_equal(getattr(b, f), getattr(c, f)), (m, f)
 
 
 def _env_run(T, hplasma, env, *args, **kw):

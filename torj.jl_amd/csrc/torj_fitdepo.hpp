@@ -671,6 +671,45 @@ TORJ_HD void fit_depo_stream(const FitArgs &a, const DepoStream &ds, int i, doub
     if (depo_windows(R, W, C, started, S)) depo_save(ds, a.n, i, W, C);
 }
 
+// The split form of one streamed window (TORJ_DEPO_STREAM=3): the elimination
+// and the walk of ray i's next window in two launches, so the elimination's
+// latency-bound rows run in a small-register kernel beside the alpha waves
+// and only the walk needs the large one.  At most one window per launch pair
+// (the windows are schedule-independent; k_depo_tail takes what is left).
+// The next window of ray i, if the scan's S steps cover it:
+TORJ_HD bool depo_next_window(const DepoStream &ds, size_t n, int i, int S, int &ja, bool &started) {
+    const int j = ds.v[kDsJ * n + i];
+    started = j >= 0;
+    ja = started ? j : 0;
+    return ja + kDepoQ + 3 + kDepoW <= S;  // depo_windows' test with last = S
+}
+// k_depo_elim: the next window's rows of the elimination
+TORJ_HD void fit_depo_stream_elim(const FitArgs &a, const DepoStream &ds, int i, double psiL, int S) {
+    if (!(a.s0[i] > 0.0)) return;
+    int ja;
+    bool started;
+    if (!depo_next_window(ds, a.n, i, S, ja, started)) return;
+    RayData R{&a, i, S + 2, a.s0[i], psiL};
+    nak_eliminate_rows(R, started ? ja + 3 : 1, ja + kDepoQ + 2 + kDepoW);
+}
+// k_depo_walk: that window's walk, after k_depo_elim on the same S
+TORJ_HD void fit_depo_stream_walk(const FitArgs &a, const DepoStream &ds, int i, double psiL, int S) {
+    if (!(a.s0[i] > 0.0)) return;
+    int ja;
+    bool started;
+    if (!depo_next_window(ds, a.n, i, S, ja, started)) return;
+    RayData R{&a, i, S + 2, a.s0[i], psiL};
+    Walker<kOpenCache> W{&a, i, 0.0, 0.0, Cursor{&a, 0, 0.0, 0.0}};
+    W.init();
+    WalkCarry C{};
+    if (started)
+        depo_load(ds, a.n, i, W, C);
+    else
+        walk_start(W, R, C);
+    walk_segments(W, R, C, ja + kDepoQ);
+    depo_save(ds, a.n, i, W, C);
+}
+
 // k_depo_tail: the windows still left, the exact rest of the ray, the finish
 TORJ_HD void fit_depo_tail(const FitArgs &a, const DepoStream &ds, int i, double psiL) {
     const int m = a.steps[i] + 2;

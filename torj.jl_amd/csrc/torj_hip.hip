@@ -1522,28 +1522,57 @@ __device__ __forceinline__ bool fit_grid_lds(FitArgs &a) {
     a.grid = s_grid;
     return true;
 }
-// s_cap: the steps whose samples this launch may read (the end of the block
-// whose scan it follows).  On its own stream (TORJ_DEPO_STREAM=2) the launch
-// can overlap the next block's scan, so sinfo may already hold that scan's
-// carry, whose samples need not be visible yet: S is capped at the block end
-// (and a ray that scan stopped is left to k_depo_tail, as any stopped ray).
-// Windows are schedule-independent (torj_fitdepo.hpp), so the outputs do not
-// depend on which carry the read saw.
-__global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds, const int *sinfo, int s_cap) {
-    fit_grid_lds(a);
-    const int i = blockIdx.x * 64 + threadIdx.x;
-    if (i >= a.n) return;
+// The windows' gate: a ray still running (a stopped one is k_depo_tail's),
+// S = its scanned steps capped at s_cap, a new window ready; psi at the launch
+// point (point 0) only for the walk's start.  s_cap: the steps whose samples
+// this launch may read (the end of the block whose scan it follows).  On its
+// own stream (TORJ_DEPO_STREAM=2) the launch can overlap the next block's
+// scan, so sinfo may already hold that scan's carry, whose samples need not
+// be visible yet: S is capped at the block end (and a ray that scan stopped is
+// left to k_depo_tail).  Windows are schedule-independent (torj_fitdepo.hpp),
+// so the outputs do not depend on which carry the read saw.
+__device__ __forceinline__ bool depo_stream_gate(const FitArgs &a, const DepoStream &ds, const int *sinfo,
+                                                 int s_cap, int i, int &S, double &psiL) {
     const int v = __hip_atomic_load(sinfo + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (info_status(v) != ST_OK) return;  // stopped: k_depo_tail takes the rest
-    const int S = min(info_steps(v), s_cap), j = ds.v[kDsJ * (size_t)a.n + i];
-    if ((j < 0 ? 0 : j) + kDepoQ + 3 + kDepoW > S) return;  // no new window yet
-    // psi at the launch point (point 0) enters only the walk's start
-    double psiL = 0.0;
+    if (info_status(v) != ST_OK) return false;
+    S = min(info_steps(v), s_cap);
+    const int j = ds.v[kDsJ * (size_t)a.n + i];
+    if ((j < 0 ? 0 : j) + kDepoQ + 3 + kDepoW > S) return false;  // no new window yet
+    psiL = 0.0;
     if (j < 0) {
         const double xl[3] = {a.x_launch[i], a.x_launch[a.n + i], a.x_launch[2 * a.n + i]};
         psiL = psi_at(a.coef, a.g, xl);
     }
+    return true;
+}
+__global__ void __launch_bounds__(64, 2) k_depo_stream(FitArgs a, DepoStream ds, const int *sinfo, int s_cap) {
+    fit_grid_lds(a);
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int S;
+    double psiL;
+    if (i >= a.n || !depo_stream_gate(a, ds, sinfo, s_cap, i, S, psiL)) return;
     fit_depo_stream(a, ds, i, psiL, S);
+}
+// TORJ_DEPO_STREAM=3: a window's elimination and walk as two launches
+// (torj_fitdepo.hpp fit_depo_stream_elim / _walk), the same S and gating
+#ifndef TORJ_DEPO_ELIM_WAVES
+#define TORJ_DEPO_ELIM_WAVES 4
+#endif
+__global__ void __launch_bounds__(64, TORJ_DEPO_ELIM_WAVES) k_depo_elim(FitArgs a, DepoStream ds, const int *sinfo,
+                                                                        int s_cap) {
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int S;
+    double psiL;
+    if (i >= a.n || !depo_stream_gate(a, ds, sinfo, s_cap, i, S, psiL)) return;
+    fit_depo_stream_elim(a, ds, i, psiL, S);
+}
+__global__ void __launch_bounds__(64, 2) k_depo_walk(FitArgs a, DepoStream ds, const int *sinfo, int s_cap) {
+    fit_grid_lds(a);
+    const int i = blockIdx.x * 64 + threadIdx.x;
+    int S;
+    double psiL;
+    if (i >= a.n || !depo_stream_gate(a, ds, sinfo, s_cap, i, S, psiL)) return;
+    fit_depo_stream_walk(a, ds, i, psiL, S);
 }
 __global__ void __launch_bounds__(64, 2) k_depo_tail(FitArgs a, DepoStream ds) {
     fit_grid_lds(a);
@@ -2623,7 +2652,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
     // TORJ_DEPO_STREAM=1: the windows on the scan's stream, after each scan;
     // =2: on a stream of their own, each after its block's scan, so the next
-    // scan (and the ring slot it releases) does not wait behind them
+    // scan (and the ring slot it releases) does not wait behind them; =3: on
+    // the scan's stream, each window's elimination and walk as two launches
     const char *dstream_e = getenv("TORJ_DEPO_STREAM");  // read per call (tests compare both)
     const int dstream_env = dstream_e ? atoi(dstream_e) : 1;
     const bool dstream = fa && dso && dstream_env != 0;
@@ -2769,8 +2799,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         // behind the alpha or the trajectory kernel's stream 3.03 / 2.98e9)
         if (dstream && b + 1 < n_blocks) {
             if (depo_own) HIPCK(hipStreamWaitEvent(sD, p->ev_S[r], 0));
-            hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
-                               sp.k0 + sp.kb);
+            if (dstream_env == 3) {  // elimination and walk as two launches
+                hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sD, *fa, ds, sp.sinfo, sp.k0 + sp.kb);
+                hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
+                                   sp.k0 + sp.kb);
+            } else {
+                hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
+                                   sp.k0 + sp.kb);
+            }
         }
     }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
