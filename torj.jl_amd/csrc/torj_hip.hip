@@ -911,10 +911,14 @@ __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st
 
 // One cold RK4 step of ray_segment's arithmetic (plasma_point with ln Te, as
 // the absorbing kernels evaluate it); STORE: this step's alpha inputs -> ain.
-template <bool STORE, int NS = kNF, class CS = const double *>
+// PSI: stage 0's stencil also sums psi at x (the step's start), returned in
+// *psi_x -- the psi the previous step's end needs (traj_run), bit for bit the
+// eval_one at that point.
+template <bool STORE, int NS = kNF, class CS = const double *, bool PSI = false>
 __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
                                           const SplitArgs &sp, int j, int i, const double x[3],
-                                          const double N[3], double xn[3], double Nn[3]) {
+                                          const double N[3], double xn[3], double Nn[3],
+                                          double *psi_x = nullptr) {
     const double hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
     double acc[6] = {0, 0, 0, 0, 0, 0}, xt[3], Nt[3], k[6];
 #pragma unroll
@@ -925,7 +929,18 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
 #pragma unroll 1
     for (int st = 0; st < 4; st++) {
         PlasmaPoint p;
-        plasma_point<true, NS>(coef, a.g, a.k, xt, p);
+        if constexpr (PSI) {
+            // stage 0 with the sixth field (a branch around whole evaluations: a
+            // per-field gate inside the stencil split its blocks and spilled)
+            if (st == 0) {
+                plasma_point<true, NS, CS, true>(coef, a.g, a.k, xt, p);
+                *psi_x = p.psi;
+            } else {
+                plasma_point<true, NS>(coef, a.g, a.k, xt, p);
+            }
+        } else {
+            plasma_point<true, NS>(coef, a.g, a.k, xt, p);
+        }
         double Npar, inv;
         dispersion_grad(p, Nt, a.mode, k, &Npar, &inv);
         if constexpr (STORE) {
@@ -1024,9 +1039,33 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
         }
     }
     const int s_end = min(a.n_steps, sp.k0 + sp.kb);
-    for (int s = steps; s < s_end; s++) {
-        double xn[3], Nn[3];
-        if (cold_step<true, NS>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn)) {
+    // psi at the end of step s - 1 is psi at x_s, which step s's stage 0 sums
+    // from its own stencil (cold_step<PSI>): the end-of-step work that needs it
+    // (make_ray's psi sample, the binned deposition's psi, the psi_exit check)
+    // runs one iteration late, before step s's outcome is looked at, so the
+    // order of stops is ray_segment's (psi check, then the next step's NaN);
+    // the block's last step takes the one eval_one left.  A ray stopped by the
+    // check has stored step s's alpha inputs too -- beyond its steps, so
+    // k_alpha_pts and the scan never read them.
+    auto step_end = [&](int k, double psi_b) -> bool {  // after step k (steps = k + 1)
+        const int sk = k + 1;
+        if constexpr (DEPO == kDepoSamples) a.smp_psi[smp_at(sk, i, a.smp_rows)] = psi_b;
+        if constexpr (DEPO == kDepoBinned) sp.psib[(size_t)(k - sp.k0) * a.n + i] = psi_b;
+        return a.chunk_steps > 0 && (sk % a.chunk_steps) == 0 && psi_b > a.psi_exit;  // src/solve.jl:174
+    };
+    const int s_first = steps;
+    bool pending = false;  // step steps - 1 still needs its psi
+    for (int s = s_first; s < s_end; s++) {
+        double xn[3], Nn[3], psi_x;
+        const bool bad = cold_step<true, NS, CS, true>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn, &psi_x);
+        if (pending) {
+            pending = false;
+            if (step_end(s - 1, psi_x)) {
+                st = ST_LEFT_PLASMA;
+                break;
+            }
+        }
+        if (bad) {
             st = ST_NAN;
             break;
         }
@@ -1037,11 +1076,7 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
         }
         steps = s + 1;
         const bool check = a.chunk_steps > 0 && (steps % a.chunk_steps) == 0;
-        double psi_b = 0.0;
-        if (DEPO != kDepoNone || check)
-            psi_b = eval_one<NS>(coef, a.g, sqrt_pos(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI);
-        if constexpr (DEPO == kDepoSamples) a.smp_psi[smp_at(steps, i, a.smp_rows)] = psi_b;
-        if constexpr (DEPO == kDepoBinned) sp.psib[(size_t)(s - sp.k0) * a.n + i] = psi_b;
+        pending = DEPO != kDepoNone || check;
         if constexpr (TRAJ) {
             if (a.traj_stride > 0 && (steps % a.traj_stride) == 0) {
                 double *T = a.traj + (size_t)(steps / a.traj_stride - 1) * 5 * a.n + i;
@@ -1058,12 +1093,10 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
                 cb[c * (size_t)a.n] = x[c];
                 cb[(3 + c) * (size_t)a.n] = N[c];
             }
-            if (psi_b > a.psi_exit) {  // src/solve.jl:174
-                st = ST_LEFT_PLASMA;
-                break;
-            }
         }
     }
+    if (pending && step_end(steps - 1, eval_one<NS>(coef, a.g, sqrt_pos(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI)))
+        st = ST_LEFT_PLASMA;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
         sp.tx[c * (size_t)a.n + i] = x[c];

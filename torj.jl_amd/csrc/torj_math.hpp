@@ -535,17 +535,30 @@ TORJ_HD Consts make_consts(double omega) {
     return c;
 }
 
-// fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te
-template <bool WITH_TE, int NS = kNF, class CS = const double *>
+// fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te.
+// WITH_PSI (the split trajectory kernel): psi as a sixth, value-only field of the
+// same stencil -- the value eval_one(coef, g, R, Z, F_PSI) gives at the same
+// point (the same R, the same per-field fma sequence) for 20 fma: the weights,
+// the cell and the (ln Te, psi) pair loads are shared
+template <bool WITH_TE, int NS = kNF, class CS = const double *, bool WITH_PSI = false>
 TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
+    static_assert(WITH_TE || !WITH_PSI, "psi rides with ln Te");
     const double R = sqrt_pos(x[0] * x[0] + x[1] * x[1]);
     const double invR = rcp_nz(R);
     const double c = x[0] * invR, s = x[1] * invR;
-    constexpr int NV = WITH_TE ? 1 : 0;
+    constexpr int NV = WITH_TE ? (WITH_PSI ? 2 : 1) : 0;
     FieldPack<4, NV> f;
     const bool in = inside_grid(g, R, x[2]);
-    if constexpr (WITH_TE) {
+    if constexpr (WITH_PSI) {
+        const int idx[6] = {F_BR, F_BPHI, F_BZ, F_LNNE, F_LNTE, F_PSI};
+        if (in)
+            eval_fields<4, 2, false, NS>(coef, g, R, x[2], idx, f);
+        else
+            eval_fields<4, 2, true, NS>(coef, g, R, x[2], idx, f);
+        p.lnTe = f.v[4];
+        p.psi = f.v[5];
+    } else if constexpr (WITH_TE) {
         const int idx[5] = {F_BR, F_BPHI, F_BZ, F_LNNE, F_LNTE};
         if (in)
             eval_fields<4, 1, false, NS>(coef, g, R, x[2], idx, f);
