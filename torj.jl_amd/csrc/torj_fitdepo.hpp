@@ -74,6 +74,10 @@ TORJ_HD int imax(int x, int y) { return x > y ? x : y; }
 
 constexpr int kChunk = 8;      // points per prefetch batch of the sequential sweeps
 constexpr int kWalkChunk = 4;  // the walk's batch (five streams, the heavy segment code)
+// the streamed walk kernel's batch (k_depo_walk, TORJ_DEPO_STREAM=3): one
+// segment at a time fits 168 VGPRs without spilling (three waves per SIMD
+// beside the alpha waves); the batch of 4 needs 244
+constexpr int kWalkChunkStream = 1;
 
 struct RayData {
     const FitArgs *a;
@@ -439,15 +443,15 @@ TORJ_HD void walk_start(W_ &W, const RayData &R, WalkCarry &C) {
 // derivatives from the upward substitution M_r = g_r - e_r M_{r-1}
 // (nak_eliminate) as it goes; rows C.j + 3 .. j_end + 2 (at most m - 2) of the
 // elimination are final
-template <class W_>
+template <int WC = kWalkChunk, class W_>
 TORJ_HD void walk_segments(W_ &W, const RayData &R, WalkCarry &C, int j_end) {
     const int m = R.m;
     double Ml = C.Ml, Mr = C.Mr, Mn = C.Mn, MPl = C.MPl, MPr = C.MPr, MPn = C.MPn;
     double yl = C.yl, Pl = C.Pl;
-    for (int j0 = C.j; j0 < j_end; j0 += kWalkChunk) {
-        double yv[kWalkChunk], Pv[kWalkChunk], ev[kWalkChunk], gv[kWalkChunk], gPv[kWalkChunk];
+    for (int j0 = C.j; j0 < j_end; j0 += WC) {
+        double yv[WC], Pv[WC], ev[WC], gv[WC], gPv[WC];
 #pragma unroll
-        for (int u = 0; u < kWalkChunk; u++) {
+        for (int u = 0; u < WC; u++) {
             const int j = imin(j0 + 1 + u, m - 1);
             yv[u] = R.Ypsi(j);
             Pv[u] = R.YP(j);
@@ -457,7 +461,7 @@ TORJ_HD void walk_segments(W_ &W, const RayData &R, WalkCarry &C, int j_end) {
             gPv[u] = R.GPP(r);
         }
 #pragma unroll
-        for (int u = 0; u < kWalkChunk; u++) {
+        for (int u = 0; u < WC; u++) {
             const int j = j0 + u;
             if (j >= j_end) break;
             const double h = R.h(j), ih = rcp_nz(h);
@@ -706,7 +710,7 @@ TORJ_HD void fit_depo_stream_walk(const FitArgs &a, const DepoStream &ds, int i,
         depo_load(ds, a.n, i, W, C);
     else
         walk_start(W, R, C);
-    walk_segments(W, R, C, ja + kDepoQ);
+    walk_segments<kWalkChunkStream>(W, R, C, ja + kDepoQ);
     depo_save(ds, a.n, i, W, C);
 }
 

@@ -1599,7 +1599,11 @@ __global__ void __launch_bounds__(64, TORJ_DEPO_ELIM_WAVES) k_depo_elim(FitArgs 
     if (i >= a.n || !depo_stream_gate(a, ds, sinfo, s_cap, i, S, psiL)) return;
     fit_depo_stream_elim(a, ds, i, psiL, S);
 }
-__global__ void __launch_bounds__(64, 2) k_depo_walk(FitArgs a, DepoStream ds, const int *sinfo, int s_cap) {
+#ifndef TORJ_DEPO_WALK_WAVES
+#define TORJ_DEPO_WALK_WAVES 3  // 168 VGPRs at kWalkChunkStream = 1, no spill
+#endif
+__global__ void __launch_bounds__(64, TORJ_DEPO_WALK_WAVES) k_depo_walk(FitArgs a, DepoStream ds, const int *sinfo,
+                                                                        int s_cap) {
     fit_grid_lds(a);
     const int i = blockIdx.x * 64 + threadIdx.x;
     int S;
@@ -2687,8 +2691,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // =2: on a stream of their own, each after its block's scan, so the next
     // scan (and the ring slot it releases) does not wait behind them; =3: on
     // the scan's stream, each window's elimination and walk as two launches
+    // (the default since round 4: DESIGN.md 3.4)
     const char *dstream_e = getenv("TORJ_DEPO_STREAM");  // read per call (tests compare both)
-    const int dstream_env = dstream_e ? atoi(dstream_e) : 1;
+    const int dstream_env = dstream_e ? atoi(dstream_e) : 3;
     const bool dstream = fa && dso && dstream_env != 0;
     const size_t b_dsd = dstream ? al(kDsNd * sizeof(double) * n) : 0,
                  b_dsi = dstream ? al(kDsNi * sizeof(int) * n) : 0;
