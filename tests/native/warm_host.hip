@@ -185,4 +185,34 @@ void fd_profile_stream(int n, int n_steps, int n_psi, double ds, const double *g
     for (size_t k = 0; k + 1 < L; k++)
         for (size_t i = 0; i < N; i++) dPs[k * N + i] = dp[k * N + i];
 }
+
+// the split trajectory kernel's field evaluations, host build: the node stencil
+// (eval_fields on kNF doubles per node) and the per-cell power form
+// (cell_power_table + eval_fields on a TileCell without a tile, i.e. the global
+// fallback of k_traj_cell) at the same points; out: n x 14 per variant (six
+// values, then dR, dZ of the four gradient fields Br, Bphi, Bz, ln ne)
+void fe_eval(int nR, int nZ, double R1, double Rn, double Z1, double Zn, const double *coef, int n,
+             const double *R, const double *Z, int cell, double *out) {
+    torj::Grid g{};
+    g.nR = nR, g.nZ = nZ, g.R1 = R1, g.Rn = Rn, g.Z1 = Z1, g.Zn = Zn;
+    g.hR = (Rn - R1) / (nR - 1), g.hZ = (Zn - Z1) / (nZ - 1);
+    g.invhR = 1.0 / g.hR, g.invhZ = 1.0 / g.hZ;
+    std::vector<double> tab;
+    if (cell) {
+        tab.resize((size_t)(nR - 1) * (nZ - 1) * torj::kCellRec);
+        torj::cell_power_table(coef, nR, nZ, tab.data());
+    }
+    const torj::TileCell tc{tab.data(), nullptr, 0, 0, 0, 0};
+    const int idx[6] = {torj::F_BR, torj::F_BPHI, torj::F_BZ, torj::F_LNNE, torj::F_LNTE, torj::F_PSI};
+    for (int k = 0; k < n; k++) {
+        torj::FieldPack<4, 2> f;
+        if (cell)
+            torj::eval_fields<4, 2, true>(tc, g, R[k], Z[k], idx, f);
+        else
+            torj::eval_fields<4, 2, true>(coef, g, R[k], Z[k], idx, f);
+        double *o = out + (size_t)k * 14;
+        for (int q = 0; q < 6; q++) o[q] = f.v[q];
+        for (int q = 0; q < 4; q++) o[6 + 2 * q] = f.dR[q], o[7 + 2 * q] = f.dZ[q];
+    }
+}
 }

@@ -87,11 +87,14 @@ def _close(a, b, tol):
     for cols in (slice(0, 3), slice(3, 6)):
         e = np.abs(sa[:, cols] - sb[:, cols]).max(1) / np.linalg.norm(sa[:, cols], axis=1)
         assert e.max() <= tol, e.max()
-    # tau: relative, with an absolute floor of 1e-14 -- rays far from any
+    # tau: relative, with an absolute floor of 1e-13 -- rays far from any
     # resonance carry tau ~ 1e-150 built from the tails of exp(-mu (gamma - 1)),
     # whose relative sensitivity to an ulp of position is ~ mu (gamma - 1)
-    # (P = 1 - tau is exact there to 1e-16 either way)
-    assert (np.abs(sa[:, 6] - sb[:, 6]) - tol * np.abs(sa[:, 6])).max() <= 1e-14
+    # (P = 1 - tau is exact there to 1e-16 either way); the split path's
+    # trajectory kernel evaluates the fields in per-cell power form (the same
+    # interpolant, other roundings: x, N within ~4e-16), which moves tau of a
+    # weakly absorbed ray by up to ~3e-14 against the fused kernels' stencil
+    assert (np.abs(sa[:, 6] - sb[:, 6]) - tol * np.abs(sa[:, 6])).max() <= 1e-13
     # the reference deposition locates each shell-boundary root of the psi(s)
     # spline; where a ray grazes a boundary (near-double root) an ulp of
     # trajectory moves the root by ~sqrt(eps), or makes a tangency a root pair

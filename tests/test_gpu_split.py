@@ -139,9 +139,13 @@ def test_split_warm_equals_fused(gpu, T, hplasma, model, n_rings):
     """The warm models on the split path (k_alpha_warm_pts: the group-velocity
     factor as a sixth stored input): the library's default for small warm beams
     (fewer groups than 3 per CU) and sched mode 3, against the fused work-queue
-    kernel: statuses and steps exact, x, N 1e-12, tau 1e-10 (measured 7e-12 /
-    4e-15), reference deposition 1e-9; the iwarm-1 work counters (integer trip
-    counts of the same alpha code) equal."""
+    kernel: statuses and steps exact, x, N 1e-12, tau 1e-10 (model 3; measured
+    4e-15) and 1e-9 (model 2: measured 7e-12 with the node stencil in both, 1.5e-10
+    since the split trajectory kernel evaluates the fields in per-cell power
+    form -- positions within ~4e-16, and iwarm 1's cold-edge root selection is
+    that sensitive: DESIGN.md 3.6, the a-priori conditioning flag of
+    tests/test_gpu_c5.py), reference deposition 1e-9; the iwarm-1 work counters
+    (integer trip counts of the same alpha code) equal."""
     import ctypes
 
     import torch
@@ -158,7 +162,7 @@ def test_split_warm_equals_fused(gpu, T, hplasma, model, n_rings):
             e = np.abs(a.state[:, cols] - r.state[:, cols]).max(1) / np.linalg.norm(a.state[:, cols], axis=1)
             assert e.max() <= 1e-12, e.max()
         assert a.state[:, 6].min() > 1.0  # the X2 layer is crossed
-        assert (np.abs(a.state[:, 6] - r.state[:, 6]) / a.state[:, 6]).max() <= 1e-10
+        assert (np.abs(a.state[:, 6] - r.state[:, 6]) / a.state[:, 6]).max() <= (1e-9 if model == 2 else 1e-10)
         assert np.abs(a.P_dep - r.P_dep).max() <= 1e-9
         assert np.abs(a.dP_shell - r.dP_shell).max() <= 1e-9 * np.abs(a.dP_shell).max()
     if model != 2:
@@ -349,41 +353,46 @@ def _env_run(T, hplasma, env, *args, **kw):
                 os.environ[k] = v
 
 
-def test_traj_tile_bit_identical_to_global_fallback(gpu, T, hplasma):
+@pytest.mark.parametrize("tile,caps", [("2", ("30", "0")), ("3", ("2", "0"))])
+def test_traj_tile_bit_identical_to_global_fallback(gpu, T, hplasma, tile, caps):
     """k_traj_tile (TORJ_TRAJ_LDS=2) stages per wave only the coefficient tile
     its rays can reach in the block and reads a stencil outside it from global
-    memory (torj_hip.hip traj_body).  The same kernel with the tile's margin at
-    0 (rays leave their tile mid-block: the per-evaluation fallback), with a
-    30-node cap (some waves untiled) and with no tile at all gives bit-identical
-    outputs; against the whole-grid LDS kernel and the L2 kernel (separately
-    compiled) to 1e-12, statuses and steps exact."""
+    memory (torj_hip.hip traj_body); k_traj_cell (=3) does the same with the
+    cells' power-form records (torj_math.hpp cell_sums).  Either kernel with the
+    tile's margin at 0 (rays leave their tile mid-block: the per-evaluation
+    fallback), with a small cap (some waves untiled) and with no tile at all
+    gives bit-identical outputs; against the whole-grid LDS kernel and the L2
+    kernel (separately compiled; for =3 also a different rounding of the same
+    interpolant) to 1e-12, statuses and steps exact."""
     from test_gpu_c3 import _close
 
     pos, xp, Np, s0, w, om = _fan(T, hplasma)
     kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, psi_grid=np.linspace(0, 1, 1000),
               deposition="reference", x_launch=pos, s0=s0)
-    ref = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": "2"}, xp, Np, om, 1, **kw)
-    for env in ({"TORJ_TILE_MARGIN": "0"}, {"TORJ_TILE_CAP": "30"}, {"TORJ_TILE_CAP": "0"}):
-        r = _env_run(T, hplasma, dict(env, TORJ_TRAJ_LDS="2"), xp, Np, om, 1, **kw)
+    ref = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": tile}, xp, Np, om, 1, **kw)
+    for env in ({"TORJ_TILE_MARGIN": "0"}, {"TORJ_TILE_CAP": caps[0]}, {"TORJ_TILE_CAP": caps[1]}):
+        r = _env_run(T, hplasma, dict(env, TORJ_TRAJ_LDS=tile), xp, Np, om, 1, **kw)
         for f in ("state", "status", "steps", "P_dep", "dP_shell"):
             assert np.array_equal(getattr(ref, f), getattr(r, f)), (env, f)
         assert np.array_equal(ref.traj, r.traj, equal_nan=True), env
     for mode in ("1", "0"):
         r = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, **kw)
         _close(ref, r, 1e-12)
-        print(f"TORJ_TRAJ_LDS={mode} vs tile: bit-identical state "
-              f"{np.array_equal(ref.state, r.state)}")
+        e = (np.abs(ref.state[:, :3] - r.state[:, :3]).max(1) / np.linalg.norm(r.state[:, :3], axis=1)).max()
+        print(f"TORJ_TRAJ_LDS={mode} vs {tile}: bit-identical state {np.array_equal(ref.state, r.state)}, "
+              f"max rel x {e:.1e}")
 
 
-def test_traj_tile_vs_oracle_with_stops(gpu, T, hplasma, oplasma):
-    """The tiled trajectory kernel against the oracle with ABSORBED and
+@pytest.mark.parametrize("tile", ["2", "3"])
+def test_traj_tile_vs_oracle_with_stops(gpu, T, hplasma, oplasma, tile):
+    """The tiled trajectory kernels against the oracle with ABSORBED and
     LEFT_PLASMA stops mid-block (as test_split_termination_vs_oracle)."""
     from test_gpu_parity import _compare_trace
 
     pos, xp, Np, s0, w, om = _fan(T, hplasma, n_rings=4)
     grid = np.linspace(0, 1, 300)
     kw = dict(ds=1e-4, n_steps=4000, chunk_steps=40, psi_grid=grid, traj_stride=50, P_min=1e-2)
-    g = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": "2", "TORJ_TILE_MARGIN": "0.5"}, xp, Np, om, 1, **kw)
+    g = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": tile, "TORJ_TILE_MARGIN": "0.5"}, xp, Np, om, 1, **kw)
     o = oplasma.trace(xp, Np, om, 1, 1e-4, 4000, chunk_steps=40, psi_grid=grid, traj_stride=50,
                       P_min=1e-2)
     _compare_trace(g, o)

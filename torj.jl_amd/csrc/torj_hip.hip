@@ -109,6 +109,7 @@ static int ensure_gl_on_device(int dev) {
 // ===========================================================================
 struct TraceArgs {
     const double *coef;
+    const double *cellp;  // the coefficients' per-cell power form (torj_math.hpp cell_power_table)
     Grid g;
     Consts k;
     double omega;
@@ -1000,13 +1001,21 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
 //              workgroup per CU, and its waves share every SIMD with the alpha
 //              waves.  A stencil outside the tile reads the global array (the
 //              same values: results bit-identical in every mode).
-enum { kTrajL2 = 0, kTrajLds = 1, kTrajTile = 2 };
+//   kTrajCell  per wave and block, the tile of CELLS its rays can reach, each
+//              cell's bicubic in power form (torj_math.hpp cell_sums: 28 fma per
+//              field with its gradient against the node stencil's 44, no basis
+//              weights); the same fallback to the global cell table.
+enum { kTrajL2 = 0, kTrajLds = 1, kTrajTile = 2, kTrajCell = 3 };
 constexpr int kTrajLdsNS = 6;
 static_assert(kTrajLdsNS == kTileNS, "LDS layouts");
 #ifndef TORJ_TILE_NODES
 #define TORJ_TILE_NODES 256  // 12 KB of LDS per wave
 #endif
 constexpr int kTileNodes = TORJ_TILE_NODES;
+#ifndef TORJ_TILE_CELLS
+#define TORJ_TILE_CELLS 20  // 15 KB of LDS per wave
+#endif
+constexpr int kTileCells = TORJ_TILE_CELLS;
 
 __device__ __forceinline__ double wave_min(double v) {
 #pragma unroll
@@ -1168,6 +1177,36 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         __syncthreads();
         if (!live) return;
         traj_run<DEPO, TRAJ, kTileNS>(a, sp, tc, i, x, N, steps, st);
+    } else if constexpr (MODE == kTrajCell) {
+        // the cells the wave's live rays can reach in the block (the node tile's
+        // box, by cell), their power-form records staged in LDS
+        __shared__ __attribute__((aligned(16))) double s_cell[kTileCells * kCellRec];
+        const double R = sqrt(x[0] * x[0] + x[1] * x[1]);
+        const double inf = __builtin_inf();
+        const double rmin = wave_min(live ? R : inf), rmax = wave_max(live ? R : -inf);
+        const double zmin = wave_min(live ? x[2] : inf), zmax = wave_max(live ? x[2] : -inf);
+        if (!(rmin <= rmax && zmin <= zmax)) return;  // no live ray in the wave (wave-uniform)
+        const double m = (double)(sp.kb + 1) * a.ds * sp.tile_margin;
+        const int iR0 = cell_index(rmin - m, a.g.R1, a.g.Rn, a.g.invhR, a.g.nR),
+                  iR1 = cell_index(rmax + m, a.g.R1, a.g.Rn, a.g.invhR, a.g.nR),
+                  iZ0 = cell_index(zmin - m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ),
+                  iZ1 = cell_index(zmax + m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ);
+        TileCell tc{a.cellp, s_cell, iR0, iZ0, iR1 - iR0 + 1, iZ1 - iZ0 + 1};
+        if (tc.cw * tc.ch > sp.tile_cap) {
+            tc.cw = tc.ch = 0;  // too wide for the tile: every cell from global memory
+        } else {
+            const int cR = a.g.nR - 1, cnt = tc.cw * tc.ch * (kCellRec / 2);
+            const Dbl2 *src = reinterpret_cast<const Dbl2 *>(a.cellp);
+            Dbl2 *dst = reinterpret_cast<Dbl2 *>(s_cell);
+            for (int k = threadIdx.x; k < cnt; k += 64) {
+                const int cell = k / (kCellRec / 2), off = k - cell * (kCellRec / 2);
+                const int zr = cell / tc.cw, rr = cell - zr * tc.cw;
+                dst[k] = src[((size_t)(iZ0 + zr) * cR + iR0 + rr) * (kCellRec / 2) + off];
+            }
+        }
+        __syncthreads();
+        if (!live) return;
+        traj_run<DEPO, TRAJ, kTileNS>(a, sp, tc, i, x, N, steps, st);
     } else if constexpr (MODE == kTrajLds) {
         extern __shared__ __attribute__((aligned(16))) double s_coef[];
         const int nodes = (a.g.nR + 2) * (a.g.nZ + 2);
@@ -1199,6 +1238,10 @@ __global__ void __launch_bounds__(512, TORJ_TRAJ_LDS_WAVES) k_traj_lds(TraceArgs
 template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_tile(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, kTrajTile>(a, sp);
+}
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArgs a, SplitArgs sp) {
+    traj_body<DEPO, TRAJ, kTrajCell>(a, sp);
 }
 
 // alpha at the stored stage points of one block: block = 256 lanes = 4 groups
@@ -1893,6 +1936,7 @@ struct torj_plasma_s {
     Grid g{};
     std::vector<double> coef;  // interleaved host copy
     double *d_coef = nullptr;
+    double *d_cellp = nullptr;  // per-cell power form of coef (the cell-tiled trajectory kernel)
     int n_vol = 0;
     double v1 = 0, vn = 0;
     std::vector<double> vol_coef;
@@ -1988,6 +2032,12 @@ static int ensure_device(torj_plasma_s *p) {
     HIPCK(hipMalloc(&p->d_coef, p->coef.size() * sizeof(double)));
     HIPCK(hipMemcpy(p->d_coef, p->coef.data(), p->coef.size() * sizeof(double),
                     hipMemcpyHostToDevice));
+    {
+        std::vector<double> cp((size_t)(p->g.nR - 1) * (p->g.nZ - 1) * kCellRec);
+        cell_power_table(p->coef.data(), p->g.nR, p->g.nZ, cp.data());
+        HIPCK(hipMalloc(&p->d_cellp, cp.size() * sizeof(double)));
+        HIPCK(hipMemcpy(p->d_cellp, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice));
+    }
     HIPCK(hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking));
     HIPCK(hipDeviceGetAttribute(&p->n_cu, hipDeviceAttributeMultiprocessorCount, p->device));
     HIPCK(hipMalloc(&p->d_flags, sizeof(int)));
@@ -2035,9 +2085,36 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         // priority, so its waves are dispatched ahead of the alpha kernel's
         int lo = 0, hi = 0;
         HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
-        HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
-        HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
+        // TORJ_TRAJ_CUS=X: the trajectory stream on X of the device's CUs (evenly
+        // spread over the mask's bits), the alpha and scan streams on the rest
+        int dev = 0, ncu = 0;
+        HIPCK(hipGetDevice(&dev));
+        HIPCK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+        const char *tc = getenv("TORJ_TRAJ_CUS"), *ac = getenv("TORJ_ALPHA_CUS");
+        const int X = tc ? atoi(tc) : 0, Y = ac ? atoi(ac) : 0;
+        if (Y > 0 && Y < ncu) {
+            // TORJ_ALPHA_CUS=Y: only the alpha and scan streams masked (to Y CUs),
+            // the trajectory stream on every CU -- the others never hold alpha waves
+            std::vector<uint32_t> mA((ncu + 31) / 32, 0u);
+            for (int c = 0; c < ncu; c++)
+                if (((long)(c + 1) * Y) / ncu != ((long)c * Y) / ncu) mA[c / 32] |= 1u << (c % 32);
+            HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
+            HIPCK(hipExtStreamCreateWithCUMask(&p->stream2, (uint32_t)mA.size(), mA.data()));
+            HIPCK(hipExtStreamCreateWithCUMask(&p->streamS, (uint32_t)mA.size(), mA.data()));
+        } else if (X > 0 && X < ncu) {
+            std::vector<uint32_t> mT((ncu + 31) / 32, 0u), mA((ncu + 31) / 32, 0u);
+            for (int c = 0; c < ncu; c++) {
+                const bool t = ((long)(c + 1) * X) / ncu != ((long)c * X) / ncu;
+                (t ? mT : mA)[c / 32] |= 1u << (c % 32);
+            }
+            HIPCK(hipExtStreamCreateWithCUMask(&p->streamT, (uint32_t)mT.size(), mT.data()));
+            HIPCK(hipExtStreamCreateWithCUMask(&p->stream2, (uint32_t)mA.size(), mA.data()));
+            HIPCK(hipExtStreamCreateWithCUMask(&p->streamS, (uint32_t)mA.size(), mA.data()));
+        } else {
+            HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
+            HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
+            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
+        }
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
             HIPCK(hipEventCreateWithFlags(&p->ev_A[q], hipEventDisableTiming));
@@ -2287,6 +2364,7 @@ int torj_plasma_destroy(torj_plasma_t p) {
     }
     if (p->stage.sc) (void)hipStreamDestroy(p->stage.sc);
     if (p->d_coef) (void)hipFree(p->d_coef);
+    if (p->d_cellp) (void)hipFree(p->d_cellp);
     if (p->stream) (void)hipStreamDestroy(p->stream);
     if (p->d_sched) (void)hipFree(p->d_sched);
     if (p->d_fit) (void)hipFree(p->d_fit);
@@ -2773,14 +2851,18 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // 61.6 ms on the headline beam; TORJ_TRAJ_LDS=0 reads them through L2)
     // (read per call: the tests compare the modes; TORJ_TILE_CAP / TORJ_TILE_MARGIN
     // shrink the tile to exercise the global-memory fallback)
+    // TORJ_TRAJ_LDS: 3 (default since round 4) the cell-tiled power-form kernel
+    // k_traj_cell (trace phase 51.4-51.5 -> 48.9-49.3 ms on the headline beam,
+    // alternating); 1 the whole-grid node table in LDS; 2 the node tile; 0 L2
     const char *lds_e = getenv("TORJ_TRAJ_LDS");
-    const int lds_env = lds_e ? atoi(lds_e) : 1;
+    const int lds_env = lds_e ? atoi(lds_e) : 3;
     const char *cap_e = getenv("TORJ_TILE_CAP"), *mar_e = getenv("TORJ_TILE_MARGIN");
-    sp.tile_cap = std::min(kTileNodes, cap_e ? atoi(cap_e) : kTileNodes);
+    const int tile_max = lds_env == 3 ? kTileCells : kTileNodes;  // cells / nodes
+    sp.tile_cap = std::min(tile_max, cap_e ? atoi(cap_e) : tile_max);
     sp.tile_margin = mar_e ? atof(mar_e) : 1.001;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
     const bool lds_traj = lds_env == 1 && lds_bytes <= 160 * 1024;
-    const bool tile_traj = lds_env == 2;
+    const bool tile_traj = lds_env == 2, cell_traj = lds_env == 3;
     const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
@@ -2806,7 +2888,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
-        if (tile_traj)
+        if (cell_traj)
+            TORJ_SPLIT_DISPATCH(k_traj_cell, dim3(G), dim3(64), 0, sT, a, sp);
+        else if (tile_traj)
             TORJ_SPLIT_DISPATCH(k_traj_tile, dim3(G), dim3(64), 0, sT, a, sp);
         else if (lds_traj)
             TORJ_SPLIT_DISPATCH(k_traj_lds, dim3(nblocks(G, wpb)), dim3(64 * wpb), lds_bytes, sT, a, sp);
@@ -3010,6 +3094,7 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     hipStream_t s = (hipStream_t)stream;
     TraceArgs a{};
     a.coef = p->d_coef;
+    a.cellp = p->d_cellp;
     a.g = p->g;
     a.k = make_consts(cfg->omega);
     a.omega = cfg->omega;

@@ -401,18 +401,30 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
     fields_finish<NGRAD, NVAL, EXT>(g, aR, aZ, v, gr, gz, grz, out);
 }
 
-// physical gradients and Line() extrapolation from the stencil sums
+// physical gradients and Line() extrapolation from the stencil sums (the
+// Line() distances dRx = R - clamp(R), dZx = Z - clamp(Z); gr, gz, grz: d/du,
+// d/dv, d2/du dv in the grid's index coordinates)
+template <int NGRAD, int NVAL, bool EXT>
+TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double *v,
+                             const double *gr, const double *gz, const double *grz,
+                             FieldPack<NGRAD, NVAL> &out);
 template <int NGRAD, int NVAL, bool EXT>
 TORJ_HD void fields_finish(const Grid &g, const Axis &aR, const Axis &aZ, const double *v,
                            const double *gr, const double *gz, const double *grz,
                            FieldPack<NGRAD, NVAL> &out) {
+    fields_finish_d<NGRAD, NVAL, EXT>(g, aR.delta, aZ.delta, v, gr, gz, grz, out);
+}
+template <int NGRAD, int NVAL, bool EXT>
+TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double *v,
+                             const double *gr, const double *gz, const double *grz,
+                             FieldPack<NGRAD, NVAL> &out) {
     constexpr int NT = NGRAD + NVAL;
-    const bool outR = aR.delta != 0.0, outZ = aZ.delta != 0.0;
+    const bool outR = dRx != 0.0, outZ = dZx != 0.0;
 #pragma unroll
     for (int f = 0; f < NT; f++) {
         const double gR = gr[f] * g.invhR, gZ = gz[f] * g.invhZ;
         if constexpr (EXT) {
-            out.v[f] = v[f] + aR.delta * gR + aZ.delta * gZ;
+            out.v[f] = v[f] + dRx * gR + dZx * gZ;
         } else {
             out.v[f] = v[f];
         }
@@ -420,14 +432,141 @@ TORJ_HD void fields_finish(const Grid &g, const Axis &aR, const Axis &aZ, const 
             const int q = f < NGRAD ? f : 0;
             if constexpr (EXT) {
                 const double gRZ = grz[f] * (g.invhR * g.invhZ);
-                out.dR[q] = outR ? gR : gR + aZ.delta * gRZ;
-                out.dZ[q] = outZ ? gZ : gZ + aR.delta * gRZ;
+                out.dR[q] = outR ? gR : gR + dZx * gRZ;
+                out.dZ[q] = outZ ? gZ : gZ + dRx * gRZ;
             } else {
                 out.dR[q] = gR;
                 out.dZ[q] = gZ;
             }
         }
     }
+}
+
+// ---------------------------------------------------------------------------
+// The bicubic of one grid cell in power form (the split pipeline's cell-tiled
+// trajectory kernel).  In cell (iR, iZ) with local coordinates
+// tR, tZ in [0, 1] (axis_setup's cell and fraction), the B-spline sum
+// sum_{b,a} wZ_b(tZ) wR_a(tR) c_{b,a} over the cell's 4 x 4 nodes is the
+// polynomial sum_{j,i} A_ji tZ^j tR^i, A = B C B^T with B the uniform cubic
+// B-spline's power-basis matrix (bweights):
+//   a0 = (c0 + 4 c1 + c2) / 6, a1 = (c2 - c0) / 2, a2 = (c0 - 2 c1 + c2) / 2,
+//   a3 = (-c0 + 3 c1 - 3 c2 + c3) / 6.
+// Built once per plasma on the host (long double, one rounding per A_ji:
+// cell_power_table), kCellRec doubles per cell: field slot f (kNF order 0..5)
+// at f * 16, A_ji at j * 4 + i.  A field with its gradient is then 4 rows of a
+// Horner value + derivative in tR (5 fma) and three Horner sums in tZ (8 fma):
+// 28 fma against the stencil's 44, no basis weights; a value-only field 15
+// against 20.  The same interpolant; the rounding differs from the stencil's
+// by ulps (x, N ~1e-15 after 2 000 steps, tests/test_gpu_split.py).
+constexpr int kCellNS = 6;
+constexpr int kCellRec = kCellNS * 16;
+struct CellAxis {
+    int i;
+    double t, delta;
+};
+// axis_setup's cell, fraction and Line() distance (the same operations)
+TORJ_HD void cell_axis(double x, double x1, double xn, double invh, int n, CellAxis &a) {
+    const double xc = clampd(x, x1, xn);
+    a.delta = x - xc;
+    const double u = (xc - x1) * invh;
+    int i = (int)floor(u);
+    i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
+    a.t = u - (double)i;
+    a.i = i;
+}
+// A wave's tile of cell records staged in LDS: cells [cR0, cR0 + cw) x
+// [cZ0, cZ0 + ch), R fastest; g: the whole table ((nR - 1) x (nZ - 1) cells).
+// cw = 0: no tile.
+struct TileCell {
+    const double *g;
+    const double *lds;
+    int cR0, cZ0, cw, ch;
+};
+template <int NGRAD, int NVAL, bool EXT, class P>
+TORJ_HD void cell_sums(P c, const CellAxis &aR, const CellAxis &aZ, const int (&fidx)[NGRAD + NVAL],
+                       double (&v)[NGRAD + NVAL], double (&gr)[NGRAD + NVAL], double (&gz)[NGRAD + NVAL],
+                       double (&grz)[NGRAD + NVAL]) {
+    constexpr int NT = NGRAD + NVAL;
+    const double tR = aR.t, tZ = aZ.t;
+#pragma unroll
+    for (int f = 0; f < NT; f++) {
+        const bool slopes = EXT || f < NGRAD;
+        const typename Pair16Ptr<P>::type A = reinterpret_cast<typename Pair16Ptr<P>::type>(c + fidx[f] * 16);
+        double p[4], d[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const Dbl2 lo = A[2 * j], hi = A[2 * j + 1];  // (a0, a1), (a2, a3) of row tZ^j
+            // value and d/dtR by one Horner pass: p = ((a3 t + a2) t + a1) t + a0
+            const double p1 = fma(hi.y, tR, hi.x);
+            const double p2 = fma(p1, tR, lo.y);
+            p[j] = fma(p2, tR, lo.x);
+            if (slopes) d[j] = fma(fma(hi.y, tR, p1), tR, p2);
+        }
+        // over tZ: V = sum_j p_j tZ^j with dV/dtZ; d/dtR the same sum of d_j
+        const double q1 = fma(p[3], tZ, p[2]);
+        const double q2 = fma(q1, tZ, p[1]);
+        v[f] = fma(q2, tZ, p[0]);
+        if (slopes) {
+            gz[f] = fma(fma(p[3], tZ, q1), tZ, q2);
+            const double r1 = fma(d[3], tZ, d[2]);
+            const double r2 = fma(r1, tZ, d[1]);
+            gr[f] = fma(r2, tZ, d[0]);
+            if (EXT && f < NGRAD) grz[f] = fma(fma(d[3], tZ, r1), tZ, r2);
+        }
+    }
+}
+template <int NGRAD, int NVAL, bool EXT = true, int NS = kNF>
+TORJ_HD void eval_fields(const TileCell &t, const Grid &g, double R, double Z,
+                         const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
+    constexpr int NT = NGRAD + NVAL;
+    CellAxis aR, aZ;
+    cell_axis(R, g.R1, g.Rn, g.invhR, g.nR, aR);
+    cell_axis(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
+    const int dR = aR.i - t.cR0, dZ = aZ.i - t.cZ0;
+    bool in = dR >= 0 && dR < t.cw && dZ >= 0 && dZ < t.ch;
+#ifdef __HIP_DEVICE_COMPILE__
+    in = __all(in);
+    using LdsP = const __attribute__((address_space(3))) double *;
+    using GlbP = const __attribute__((address_space(1))) double *;
+#else
+    using LdsP = const double *;
+    using GlbP = const double *;
+#endif
+    double v[NT], gr[NT], gz[NT], grz[NT];
+#pragma unroll
+    for (int f = 0; f < NT; f++) gr[f] = gz[f] = grz[f] = 0.0;
+    if (in)
+        cell_sums<NGRAD, NVAL, EXT, LdsP>((LdsP)t.lds + (size_t)(dZ * t.cw + dR) * kCellRec, aR, aZ, fidx, v,
+                                          gr, gz, grz);
+    else
+        cell_sums<NGRAD, NVAL, EXT, GlbP>((GlbP)t.g + ((size_t)aZ.i * (g.nR - 1) + aR.i) * kCellRec, aR, aZ,
+                                          fidx, v, gr, gz, grz);
+    fields_finish_d<NGRAD, NVAL, EXT>(g, aR.delta, aZ.delta, v, gr, gz, grz, out);
+}
+// the cell records of a plasma's node coefficients (kNF doubles per node,
+// (nR + 2) x (nZ + 2) nodes) -> (nR - 1) x (nZ - 1) x kCellRec doubles
+inline void cell_power_table(const double *coef, int nR, int nZ, double *out) {
+    const long double s6 = 1.0L / 6.0L;
+    const long double B[4][4] = {{s6, 4 * s6, s6, 0.0L},
+                                 {-0.5L, 0.0L, 0.5L, 0.0L},
+                                 {0.5L, -1.0L, 0.5L, 0.0L},
+                                 {-s6, 0.5L, -0.5L, s6}};
+    const int mR = nR + 2;
+    for (int iZ = 0; iZ < nZ - 1; iZ++)
+        for (int iR = 0; iR < nR - 1; iR++)
+            for (int f = 0; f < kCellNS; f++) {
+                long double C[4][4];
+                for (int b = 0; b < 4; b++)
+                    for (int a = 0; a < 4; a++) C[b][a] = coef[((size_t)(iZ + b) * mR + iR + a) * kNF + f];
+                double *o = out + ((size_t)iZ * (nR - 1) + iR) * kCellRec + f * 16;
+                for (int j = 0; j < 4; j++)
+                    for (int i = 0; i < 4; i++) {
+                        long double acc = 0.0L;
+                        for (int b = 0; b < 4; b++)
+                            for (int a = 0; a < 4; a++) acc += B[j][b] * B[i][a] * C[b][a];
+                        o[j * 4 + i] = (double)acc;
+                    }
+            }
 }
 
 // Both coordinates inside the grid (no Line() extrapolation), for the whole
