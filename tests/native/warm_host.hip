@@ -200,7 +200,7 @@ void fe_eval(int nR, int nZ, double R1, double Rn, double Z1, double Zn, const d
     std::vector<double> tab;
     if (cell) {
         tab.resize((size_t)(nR - 1) * (nZ - 1) * torj::kCellRec);
-        torj::cell_power_table(coef, nR, nZ, tab.data());
+        torj::cell_power_table(coef, nR, nZ, g.hR, g.hZ, tab.data());
     }
     const torj::TileCell tc{tab.data(), nullptr, 0, 0, 0, 0};
     const int idx[6] = {torj::F_BR, torj::F_BPHI, torj::F_BZ, torj::F_LNNE, torj::F_LNTE, torj::F_PSI};

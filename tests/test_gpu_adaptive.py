@@ -57,11 +57,17 @@ def test_adaptive_step_control_engaged(gpu, T, hplasma, oplasma, fan_states):
     # whether the last proposed step lands within rounding of a chunk end: a
     # ray may take one step more or less than the oracle (different pow, fma
     # contraction), and then agrees to the integration tolerance only
+    # (or the same number of steps with an accepted step size decided the other
+    # way at EEst ~ 1: such a ray agrees to ~1e-10, the step-size rounding of
+    # the controller amplified by the error-limited steps): same-count rays to
+    # 1e-9, every ray to 1e-7
     assert np.array_equal(g.status, o["status"])
     same = g.steps == o["steps"]
     assert same.mean() > 0.75 and np.abs(g.steps - o["steps"]).max() <= 2
     ex = np.abs(g.state[:, :6] - o["state"][:, :6]).max(1) / np.abs(o["state"][:, :6]).max(1)
-    assert ex[same].max() < 1e-10 and ex.max() < 1e-7
+    assert ex[same].max() < 1e-9 and ex.max() < 1e-7, (ex[same].max(), ex.max())
+    print(f"adaptive dtmax 5 mm: {same.mean():.2f} same step count (max rel {ex[same].max():.1e}, "
+          f"median {np.median(ex[same]):.1e}), all rays {ex.max():.1e}")
     ds = np.diff(g.traj[0, :g.steps[0], 4])
     assert ds.min() < 0.5 * ds.max()  # genuinely variable steps
     assert g.steps.max() > 100

@@ -1104,7 +1104,8 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
             }
         }
     }
-    if (pending && step_end(steps - 1, eval_one<NS>(coef, a.g, sqrt_pos(x[0] * x[0] + x[1] * x[1]), x[2], F_PSI)))
+    double invR;
+    if (pending && step_end(steps - 1, eval_one<NS>(coef, a.g, cyl_radius(x, invR), x[2], F_PSI)))
         st = ST_LEFT_PLASMA;
 #pragma unroll
     for (int c = 0; c < 3; c++) {
@@ -2034,7 +2035,7 @@ static int ensure_device(torj_plasma_s *p) {
                     hipMemcpyHostToDevice));
     {
         std::vector<double> cp((size_t)(p->g.nR - 1) * (p->g.nZ - 1) * kCellRec);
-        cell_power_table(p->coef.data(), p->g.nR, p->g.nZ, cp.data());
+        cell_power_table(p->coef.data(), p->g.nR, p->g.nZ, p->g.hR, p->g.hZ, cp.data());
         HIPCK(hipMalloc(&p->d_cellp, cp.size() * sizeof(double)));
         HIPCK(hipMemcpy(p->d_cellp, cp.data(), cp.size() * sizeof(double), hipMemcpyHostToDevice));
     }

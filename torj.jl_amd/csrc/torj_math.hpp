@@ -103,6 +103,23 @@ TORJ_HD double sqrt_pos(double x) {
 #endif
 }
 
+// 1/sqrt(x) of a finite positive normal argument: v_rsq_f64 + two Newton steps
+// (~1 ulp; 9 VALU against sqrt_pos + rcp_nz's 13 where only the reciprocal is
+// needed, 10 with x * rsqrt_pos(x) where both are)
+// (the host build runs the same Newton steps after an exact 1/sqrt, so host
+// and device agree on the special operands: NaN at 0, inf, negative, NaN)
+TORJ_HD double rsqrt_pos(double x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    double y = __builtin_amdgcn_rsq(x);
+#else
+    double y = 1.0 / sqrt(x);
+#endif
+    double e = fma(-x * y, y, 1.0);
+    y = fma(0.5 * y, e, y);
+    e = fma(-x * y, y, 1.0);
+    return fma(0.5 * y, e, y);
+}
+
 // sqrt for the absorption prologue and the harmonic setup: sqrt_pos plus the
 // library's results at +-0 and +inf (a v_cmp_class and a select instead of the
 // library's scaling, two Newton corrections and class fix-up: 11 VALU against
@@ -404,7 +421,7 @@ TORJ_HD void eval_fields(const double *__restrict__ coef, const Grid &g, double 
 // physical gradients and Line() extrapolation from the stencil sums (the
 // Line() distances dRx = R - clamp(R), dZx = Z - clamp(Z); gr, gz, grz: d/du,
 // d/dv, d2/du dv in the grid's index coordinates)
-template <int NGRAD, int NVAL, bool EXT>
+template <int NGRAD, int NVAL, bool EXT, bool PHYS = false>
 TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double *v,
                              const double *gr, const double *gz, const double *grz,
                              FieldPack<NGRAD, NVAL> &out);
@@ -414,7 +431,8 @@ TORJ_HD void fields_finish(const Grid &g, const Axis &aR, const Axis &aZ, const 
                            FieldPack<NGRAD, NVAL> &out) {
     fields_finish_d<NGRAD, NVAL, EXT>(g, aR.delta, aZ.delta, v, gr, gz, grz, out);
 }
-template <int NGRAD, int NVAL, bool EXT>
+// PHYS: gr, gz, grz are already per metre (the cell records' scaled form)
+template <int NGRAD, int NVAL, bool EXT, bool PHYS>
 TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double *v,
                              const double *gr, const double *gz, const double *grz,
                              FieldPack<NGRAD, NVAL> &out) {
@@ -422,7 +440,7 @@ TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double
     const bool outR = dRx != 0.0, outZ = dZx != 0.0;
 #pragma unroll
     for (int f = 0; f < NT; f++) {
-        const double gR = gr[f] * g.invhR, gZ = gz[f] * g.invhZ;
+        const double gR = PHYS ? gr[f] : gr[f] * g.invhR, gZ = PHYS ? gz[f] : gz[f] * g.invhZ;
         if constexpr (EXT) {
             out.v[f] = v[f] + dRx * gR + dZx * gZ;
         } else {
@@ -431,7 +449,7 @@ TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double
         if (f < NGRAD) {
             const int q = f < NGRAD ? f : 0;
             if constexpr (EXT) {
-                const double gRZ = grz[f] * (g.invhR * g.invhZ);
+                const double gRZ = PHYS ? grz[f] : grz[f] * (g.invhR * g.invhZ);
                 out.dR[q] = outR ? gR : gR + dZx * gRZ;
                 out.dZ[q] = outZ ? gZ : gZ + dRx * gRZ;
             } else {
@@ -448,7 +466,9 @@ TORJ_HD void fields_finish_d(const Grid &g, double dRx, double dZx, const double
 // tR, tZ in [0, 1] (axis_setup's cell and fraction), the B-spline sum
 // sum_{b,a} wZ_b(tZ) wR_a(tR) c_{b,a} over the cell's 4 x 4 nodes is the
 // polynomial sum_{j,i} A_ji tZ^j tR^i, A = B C B^T with B the uniform cubic
-// B-spline's power-basis matrix (bweights):
+// B-spline's power-basis matrix (bweights), stored per metre: A_ji / (hR^i hZ^j)
+// in the offsets sR = tR hR, sZ = tZ hZ from the cell's corner, so the
+// derivatives come out per metre (no 1/h scaling per field):
 //   a0 = (c0 + 4 c1 + c2) / 6, a1 = (c2 - c0) / 2, a2 = (c0 - 2 c1 + c2) / 2,
 //   a3 = (-c0 + 3 c1 - 3 c2 + c3) / 6.
 // Built once per plasma on the host (long double, one rounding per A_ji:
@@ -462,16 +482,16 @@ constexpr int kCellNS = 6;
 constexpr int kCellRec = kCellNS * 16;
 struct CellAxis {
     int i;
-    double t, delta;
+    double t, delta;  // t: the offset from the cell's corner in metres
 };
-// axis_setup's cell, fraction and Line() distance (the same operations)
-TORJ_HD void cell_axis(double x, double x1, double xn, double invh, int n, CellAxis &a) {
+// axis_setup's cell, fraction (times h) and Line() distance
+TORJ_HD void cell_axis(double x, double x1, double xn, double h, double invh, int n, CellAxis &a) {
     const double xc = clampd(x, x1, xn);
     a.delta = x - xc;
     const double u = (xc - x1) * invh;
     int i = (int)floor(u);
     i = i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
-    a.t = u - (double)i;
+    a.t = (u - (double)i) * h;
     a.i = i;
 }
 // A wave's tile of cell records staged in LDS: cells [cR0, cR0 + cw) x
@@ -520,8 +540,8 @@ TORJ_HD void eval_fields(const TileCell &t, const Grid &g, double R, double Z,
                          const int (&fidx)[NGRAD + NVAL], FieldPack<NGRAD, NVAL> &out) {
     constexpr int NT = NGRAD + NVAL;
     CellAxis aR, aZ;
-    cell_axis(R, g.R1, g.Rn, g.invhR, g.nR, aR);
-    cell_axis(Z, g.Z1, g.Zn, g.invhZ, g.nZ, aZ);
+    cell_axis(R, g.R1, g.Rn, g.hR, g.invhR, g.nR, aR);
+    cell_axis(Z, g.Z1, g.Zn, g.hZ, g.invhZ, g.nZ, aZ);
     const int dR = aR.i - t.cR0, dZ = aZ.i - t.cZ0;
     bool in = dR >= 0 && dR < t.cw && dZ >= 0 && dZ < t.ch;
 #ifdef __HIP_DEVICE_COMPILE__
@@ -541,11 +561,11 @@ TORJ_HD void eval_fields(const TileCell &t, const Grid &g, double R, double Z,
     else
         cell_sums<NGRAD, NVAL, EXT, GlbP>((GlbP)t.g + ((size_t)aZ.i * (g.nR - 1) + aR.i) * kCellRec, aR, aZ,
                                           fidx, v, gr, gz, grz);
-    fields_finish_d<NGRAD, NVAL, EXT>(g, aR.delta, aZ.delta, v, gr, gz, grz, out);
+    fields_finish_d<NGRAD, NVAL, EXT, true>(g, aR.delta, aZ.delta, v, gr, gz, grz, out);
 }
 // the cell records of a plasma's node coefficients (kNF doubles per node,
 // (nR + 2) x (nZ + 2) nodes) -> (nR - 1) x (nZ - 1) x kCellRec doubles
-inline void cell_power_table(const double *coef, int nR, int nZ, double *out) {
+inline void cell_power_table(const double *coef, int nR, int nZ, double hR, double hZ, double *out) {
     const long double s6 = 1.0L / 6.0L;
     const long double B[4][4] = {{s6, 4 * s6, s6, 0.0L},
                                  {-0.5L, 0.0L, 0.5L, 0.0L},
@@ -564,6 +584,8 @@ inline void cell_power_table(const double *coef, int nR, int nZ, double *out) {
                         long double acc = 0.0L;
                         for (int b = 0; b < 4; b++)
                             for (int a = 0; a < 4; a++) acc += B[j][b] * B[i][a] * C[b][a];
+                        for (int k = 0; k < i; k++) acc /= (long double)hR;
+                        for (int k = 0; k < j; k++) acc /= (long double)hZ;
                         o[j * 4 + i] = (double)acc;
                     }
             }
@@ -625,7 +647,13 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
     const double Np2 = Npar * Npar, Y2 = Y * Y, invY = rcp_nz(Y), invY2 = invY * invY;
     const double om = 1.0 - Np2, omX = 1.0 - X;
     const double Delta = om * om + 4.0 * Np2 * omX * invY2;
-    const double sq = sqrt_nn(Delta);
+    // sqrt(Delta) and 1 / sqrt(Delta) from one rsqrt (Delta > 0 for X < 1);
+    // at +-0 and +inf sqrt keeps its value and 1 / sqrt is NaN, as rcp_nz of it
+    const double rsq = rsqrt_pos(Delta);
+    double sq = Delta * rsq;
+#ifdef __HIP_DEVICE_COMPILE__
+    if (__builtin_amdgcn_class(Delta, 0x260)) sq = Delta;
+#endif
     const double A = 1.0 + md * sq + Np2;
     const double Q = 2.0 * (-1.0 + X + Y2);
     const double invQ = rcp_nz(Q);
@@ -633,7 +661,7 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
     const double dDel_dX = -4.0 * Np2 * invY2;
     const double dDel_dY = -8.0 * Np2 * omX * invY2 * invY;
     const double dDel_dNp = -4.0 * Npar * om + 8.0 * Npar * omX * invY2;
-    const double h = md * 0.5 * rcp_nz(sq);
+    const double h = md * 0.5 * rsq;
     const double dA_dX = h * dDel_dX, dA_dY = h * dDel_dY, dA_dNp = h * dDel_dNp + 2.0 * Npar;
     const double invQ2 = invQ * invQ;
     const double dG_dX = 2.0 * Y2 * (Y2 - 1.0) * invQ2;
@@ -674,6 +702,15 @@ TORJ_HD Consts make_consts(double omega) {
     return c;
 }
 
+// R = hypot(x, y) and 1 / R of a point (plasma_point's; the split trajectory
+// kernel's step-end psi takes the same R, so psi from a stage-0 stencil and
+// from eval_one at that point are the same bits)
+TORJ_HD double cyl_radius(const double x[3], double &invR) {
+    const double R2 = x[0] * x[0] + x[1] * x[1];
+    invR = rsqrt_pos(R2);
+    return R2 * invR;
+}
+
 // fields needed by the ray RHS: 4 with gradients (Br, Bphi, Bz, ln ne) + ln Te.
 // WITH_PSI (the split trajectory kernel): psi as a sixth, value-only field of the
 // same stencil -- the value eval_one(coef, g, R, Z, F_PSI) gives at the same
@@ -683,8 +720,8 @@ template <bool WITH_TE, int NS = kNF, class CS = const double *, bool WITH_PSI =
 TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
                           const double x[3], PlasmaPoint &p) {
     static_assert(WITH_TE || !WITH_PSI, "psi rides with ln Te");
-    const double R = sqrt_pos(x[0] * x[0] + x[1] * x[1]);
-    const double invR = rcp_nz(R);
+    double invR;
+    const double R = cyl_radius(x, invR);
     const double c = x[0] * invR, s = x[1] * invR;
     constexpr int NV = WITH_TE ? (WITH_PSI ? 2 : 1) : 0;
     FieldPack<4, NV> f;
@@ -728,8 +765,8 @@ TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
     p.B[0] = Bx;
     p.B[1] = By;
     p.B[2] = Bz;
-    const double Babs = sqrt_pos(Bx * Bx + By * By + Bz * Bz);
-    const double invB = rcp_nz(Babs);
+    const double B2 = Bx * Bx + By * By + Bz * Bz;
+    const double invB = rsqrt_pos(B2), Babs = B2 * invB;
     p.Babs = Babs;
     p.invB = invB;
     p.b[0] = Bx * invB;
@@ -778,8 +815,7 @@ TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode
     const double DZ = gX * p.dlnZ + gY * p.dBabsZ + ns.dNp * UZ;
     const double DW = ns.dNp * W;
     const double dDdx[3] = {-(p.c * DR + p.s * DW), -(p.s * DR - p.c * DW), -DZ};
-    const double nrm = sqrt_pos(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
-    const double inv = rcp_nz(nrm);
+    const double inv = rsqrt_pos(dDdN[0] * dDdN[0] + dDdN[1] * dDdN[1] + dDdN[2] * dDdN[2]);
     if (inv_out) *inv_out = inv;
 #pragma unroll
     for (int q = 0; q < 3; q++) {
@@ -1052,7 +1088,7 @@ struct HarmGeom {
     bool zero;
 };
 
-TORJ_HD HarmGeom harm_geom(double mu, double r, double Npar, double inv_sqNp) {
+TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, double inv_sqNp) {
     HarmGeom g;
     g.r = r;
     g.r2m1 = r * r - 1.0;
@@ -1075,7 +1111,10 @@ TORJ_HD HarmGeom harm_geom(double mu, double r, double Npar, double inv_sqNp) {
     const double tv = -g.C2 * 0.5 * rcp_nz(g.C1);          // vertex (C1 > 0)
     const double qv = fma(-0.25 * g.C2, g.C2 * rcp_nz(g.C1), g.C0);
     g.qmin = (g.C1 > 0.0 && fabs(tv) <= 1.0) ? qv : qe;
-    g.zero = g.qmin > 1.0 && mu * (sqrt_nn(g.qmin) - 1.0) > 760.0;
+    // mu (sqrt(qmin) - 1) > 760 as qmin > (1 + 760 / mu)^2 (no square root;
+    // the threshold's few roundings are ~1e-15 of it, inside the margin of 14)
+    const double th = fma(760.0, inv_mu, 1.0);
+    g.zero = g.qmin > 1.0 && g.qmin > th * th;
     return g;
 }
 
@@ -1232,7 +1271,7 @@ TORJ_HD AlbPre albajar_pre(double Y, double N_abs, double N_par, double Te) {
     const double omNp2 = 1.0 - N_par * N_par;
     p.sqNp = sqrt_nn(omNp2);
     p.m_0 = p.sqNp * p.omega_bar;
-    p.inv_sqNp = rcp_nz(p.sqNp);
+    p.inv_sqNp = rsqrt_pos(omNp2);  // NaN where rcp_nz(sqNp) is (1 - N_par^2 <= 0, NaN)
     p.inv_m0 = p.inv_sqNp * Y;
     return p;
 }
@@ -1280,7 +1319,7 @@ TORJ_HD AlbPro albajar_prologue(const AlbPre &pre, double X, double Y, double N_
         const double ta = 1.0 + (omX * Nt2 * c2) * (inv_den * inv_den) * gg;
         const double tb = 1.0 + (omX * inv_den) * gg;
         const double a_sq = s2 * (ta * ta), b_sq = c2 * (tb * tb);
-        ea = sqrt_pos(inv_Nt * rcp_nz(sqrt_pos(a_sq + b_sq)));
+        ea = sqrt_pos(inv_Nt * rsqrt_pos(a_sq + b_sq));
         if (mode <= 0) ea = -ea;
         e1 = -(omega_bar * g) * ea;
         e3 = -((Nt2 * sin_t * cos_t) * inv_den) * e1;
@@ -1326,8 +1365,8 @@ TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, 
     const AlbPre pre = albajar_pre(Y, N_abs, N_par, Te);
     const bool h2 = !(2.0 < pre.m_0), h3 = !(3.0 < pre.m_0);  // harmonic m present iff m >= m_0
     HarmGeom g2{}, g3{};
-    if (h2) g2 = harm_geom(pre.mu, 2.0 * pre.inv_m0, N_par, pre.inv_sqNp);
-    if (h3) g3 = harm_geom(pre.mu, 3.0 * pre.inv_m0, N_par, pre.inv_sqNp);
+    if (h2) g2 = harm_geom(pre.mu, pre.inv_mu, 2.0 * pre.inv_m0, N_par, pre.inv_sqNp);
+    if (h3) g3 = harm_geom(pre.mu, pre.inv_mu, 3.0 * pre.inv_m0, N_par, pre.inv_sqNp);
     // Settled before the polarisation vector: when every harmonic present is an
     // exact zero (harm_geom), alpha is a zero whatever the polarisation -- the
     // harmonics would return -mu Pm^2 0 sq_r, finite and zero because N_perp and
