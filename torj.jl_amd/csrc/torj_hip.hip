@@ -1192,18 +1192,22 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
                   iR1 = cell_index(rmax + m, a.g.R1, a.g.Rn, a.g.invhR, a.g.nR),
                   iZ0 = cell_index(zmin - m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ),
                   iZ1 = cell_index(zmax + m, a.g.Z1, a.g.Zn, a.g.invhZ, a.g.nZ);
-        TileCell tc{a.cellp, s_cell, iR0, iZ0, iR1 - iR0 + 1, iZ1 - iZ0 + 1};
-        if (tc.cw * tc.ch > sp.tile_cap) {
+        // the box is wave-uniform: scalar registers for the copy's loop
+        const int cR0 = __builtin_amdgcn_readfirstlane(iR0), cZ0 = __builtin_amdgcn_readfirstlane(iZ0);
+        const int cw = __builtin_amdgcn_readfirstlane(iR1 - iR0 + 1), ch = __builtin_amdgcn_readfirstlane(iZ1 - iZ0 + 1);
+        TileCell tc{a.cellp, s_cell, cR0, cZ0, cw, ch};
+        if (cw * ch > sp.tile_cap) {
             tc.cw = tc.ch = 0;  // too wide for the tile: every cell from global memory
         } else {
-            const int cR = a.g.nR - 1, cnt = tc.cw * tc.ch * (kCellRec / 2);
+            // one cell record (48 x 16 B) per pass, lanes 0..47
+            const int cR = a.g.nR - 1;
             const Dbl2 *src = reinterpret_cast<const Dbl2 *>(a.cellp);
             Dbl2 *dst = reinterpret_cast<Dbl2 *>(s_cell);
-            for (int k = threadIdx.x; k < cnt; k += 64) {
-                const int cell = k / (kCellRec / 2), off = k - cell * (kCellRec / 2);
-                const int zr = cell / tc.cw, rr = cell - zr * tc.cw;
-                dst[k] = src[((size_t)(iZ0 + zr) * cR + iR0 + rr) * (kCellRec / 2) + off];
-            }
+            for (int zr = 0; zr < ch; zr++)
+                for (int rr = 0; rr < cw; rr++)
+                    if (threadIdx.x < kCellRec / 2)
+                        dst[(zr * cw + rr) * (kCellRec / 2) + threadIdx.x] =
+                            src[((size_t)(cZ0 + zr) * cR + cR0 + rr) * (kCellRec / 2) + threadIdx.x];
         }
         __syncthreads();
         if (!live) return;

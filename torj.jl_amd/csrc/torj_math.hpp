@@ -188,11 +188,13 @@ TORJ_HD double exp_fast(double x) {
 // per-harmonic constant, so y costs the one fma the natural exponent did).
 // k = round(y) by the 1.5 * 2^52 shifter (k in the low word of kd: no v_rndne,
 // no v_cvt), r = y - k exact (Sterbenz, |r| <= 1/2), and a degree-9
-// near-minimax polynomial for 2^r: exp's on |x| <= ln2/2 (tools/gen_exp_poly.py
-// 9: 333 ulp, 7.4e-14 relative) with its coefficients scaled by ln2^i.  Each
-// node term carries it once; the harmonic sum stays within ~1e-13 of the libm
-// one, three orders under the 1e-10 parity bar.  13 VALU against exp_fast's
-// 17: 3 for the reduction instead of 5, degree 9 instead of 11.  Exact for |y| < 2^51;
+// near-minimax polynomial for 2^r: exp's on |x| <= ln2/2 (round 4: degree 8,
+// tools/gen_exp_poly.py 8: 4.3e-12 relative; degree 9 before, 7.4e-14) with its
+// coefficients scaled by ln2^i.  Each node term carries it once; over 100 000
+// random tuples alpha's median error against the libm oracle is 3e-13 (2e-14
+// at degree 9), p99 2.9e-12 (1.8e-12), all under the 1e-10 parity bar but the
+// conditioning-limited few.  12 VALU against exp_fast's 17: 3
+// for the reduction instead of 5, degree 8 instead of 11.  Exact for |y| < 2^51;
 // node arguments have mu = m_e c^2 / Te < 25 550 (Te >= 20 eV,
 // src/absorption.jl:194).  Every node of a lane the exact-zero bound skips has
 // y < -1096 and gives exactly +0, so the skip stays bit-identical.
@@ -200,14 +202,13 @@ TORJ_HD double exp2_node(double y) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double kd = y + 0x1.8p52;
     const double r = y - (kd - 0x1.8p52);
-    double p = 1.0200337248760112e-07;
-    p = fma(p, r, 1.325080551750225e-06);
-    p = fma(p, r, 1.5252699025121892e-05);
-    p = fma(p, r, 0.00015403475186530786);
-    p = fma(p, r, 0.0013333558163820172);
-    p = fma(p, r, 0.00961812913523614);
-    p = fma(p, r, 0.05550410866480799);
-    p = fma(p, r, 0.24022650695888503);
+    double p = 1.3246387161221642e-06;
+    p = fma(p, r, 1.5297323760701075e-05);
+    p = fma(p, r, 0.00015403491754738786);
+    p = fma(p, r, 0.0013333502386162772);
+    p = fma(p, r, 0.009618129119704426);
+    p = fma(p, r, 0.055504108839096185);
+    p = fma(p, r, 0.24022650695910072);
     p = fma(p, r, 0.6931471805599453);
     p = fma(p, r, 1.0);
     const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, kd);  // k, low word
@@ -642,9 +643,12 @@ struct NsPartials {
     double Ns2, dX, dY, dNp;
 };
 
-TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar, int mode) {
+// invY: 1 / Y when the caller has it (dispersion_grad: 1 / |B| times 1 / Cy),
+// else 0 (one reciprocal here)
+TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar, int mode, double invY = 0.0) {
     const double md = (double)mode;
-    const double Np2 = Npar * Npar, Y2 = Y * Y, invY = rcp_nz(Y), invY2 = invY * invY;
+    if (invY == 0.0) invY = rcp_nz(Y);
+    const double Np2 = Npar * Npar, Y2 = Y * Y, invY2 = invY * invY;
     const double om = 1.0 - Np2, omX = 1.0 - X;
     const double Delta = om * om + 4.0 * Np2 * omX * invY2;
     // sqrt(Delta) and 1 / sqrt(Delta) from one rsqrt (Delta > 0 for X < 1);
@@ -688,17 +692,20 @@ struct PlasmaPoint {
     double dBabsR, dBabsZ;     // d|B|/dR, d|B|/dZ
     double dlnR, dlnZ;         // d ln ne / dR, d ln ne / dZ
     double Cy;                 // Y = |B| Cy
+    double invCy;              // 1 / Cy
 };
 
 struct Consts {
     double Cx;  // X = ne * Cx
     double Cy;  // Y = |B| * Cy
+    double invCy;
 };
 
 TORJ_HD Consts make_consts(double omega) {
     Consts c;
     c.Cx = kE * kE / (kEps0 * kMe * omega * omega);
     c.Cy = kE / (kMe * omega);
+    c.invCy = (kMe * omega) / kE;
     return c;
 }
 
@@ -777,6 +784,7 @@ TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
     p.X = ne * k.Cx;
     p.Y = Babs * k.Cy;
     p.Cy = k.Cy;
+    p.invCy = k.invCy;
     p.dlnR = f.dR[3];
     p.dlnZ = f.dZ[3];
     // d|B| = (B_cyl . dB_cyl) / |B|: |B| is axisymmetric (no tangential term)
@@ -798,7 +806,7 @@ TORJ_HD void plasma_point(CS coef, const Grid &g, const Consts &k,
 TORJ_HD double dispersion_grad(const PlasmaPoint &p, const double N[3], int mode, double du[6],
                                double *Npar_out, double *inv_out = nullptr) {
     const double Npar = N[0] * p.b[0] + N[1] * p.b[1] + N[2] * p.b[2];
-    const NsPartials ns = refractive_index_sq_partials(p.X, p.Y, Npar, mode);
+    const NsPartials ns = refractive_index_sq_partials(p.X, p.Y, Npar, mode, p.invB * p.invCy);
     const double N2 = N[0] * N[0] + N[1] * N[1] + N[2] * N[2];
     double dDdN[3];
 #pragma unroll
