@@ -1259,10 +1259,14 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArg
 // uncounted one carries no work struct at all (with its address taken
 // conditionally it lived in scratch: 32 B of stores per lane and point, ~25 GB
 // per headline launch)
+#ifndef TORJ_ALPHA_BLOCK
+#define TORJ_ALPHA_BLOCK 256  // lanes per alpha workgroup (groups of 64 rays at one (step, stage))
+#endif
+constexpr int kAlphaBlock = TORJ_ALPHA_BLOCK;
 template <bool COUNT>
-__global__ void __launch_bounds__(256, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
+__global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
     const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
-    const int i = q * 256 + threadIdx.x;
+    const int i = q * kAlphaBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
     const int ti = sp.tinfo[i];
@@ -2904,14 +2908,16 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         HIPCK(hipEventRecord(p->ev_T[r], sT));
         HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
         const dim3 agrid((unsigned)(nq * 4 * sp.kb));
+        const int nqA = (int)((n + kAlphaBlock - 1) / kAlphaBlock);
+        const dim3 agridA((unsigned)(nqA * 4 * sp.kb));
         if (a.abs_model == 3)
             hipLaunchKernelGGL(k_alpha_warm_pts<3>, agrid, dim3(256), 0, s2, a, sp, nq);
         else if (a.abs_model == 2)
             hipLaunchKernelGGL(k_alpha_warm_pts<1>, agrid, dim3(256), 0, s2, a, sp, nq);
         else if (sp.awork)  // a counted launch
-            hipLaunchKernelGGL(k_alpha_pts<true>, agrid, dim3(256), 0, s2, a, sp, nq);
+            hipLaunchKernelGGL(k_alpha_pts<true>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         else
-            hipLaunchKernelGGL(k_alpha_pts<false>, agrid, dim3(256), 0, s2, a, sp, nq);
+            hipLaunchKernelGGL(k_alpha_pts<false>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         HIPCK(hipEventRecord(p->ev_A[r], s2));
         if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_A[r], 0));
         if (a.counters)
