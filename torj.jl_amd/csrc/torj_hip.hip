@@ -1260,7 +1260,9 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArg
 // conditionally it lived in scratch: 32 B of stores per lane and point, ~25 GB
 // per headline launch)
 #ifndef TORJ_ALPHA_BLOCK
-#define TORJ_ALPHA_BLOCK 256  // lanes per alpha workgroup (groups of 64 rays at one (step, stage))
+#define TORJ_ALPHA_BLOCK 128  // lanes per alpha workgroup (groups of 64 rays at one (step, stage)): two
+// waves, placed beside the trajectory waves SIMD pair by SIMD pair (256: 47.4-47.8 ms
+// trace phase, 128: 45.6-45.7, 64: 46.7-48.6 alternating)
 #endif
 constexpr int kAlphaBlock = TORJ_ALPHA_BLOCK;
 template <bool COUNT>
