@@ -1303,11 +1303,15 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 #ifndef TORJ_WARM3_ALPHA_WAVES
 #define TORJ_WARM3_ALPHA_WAVES 1
 #endif
+#ifndef TORJ_ALPHA_WARM_BLOCK
+#define TORJ_ALPHA_WARM_BLOCK 256  // lanes per warm-alpha workgroup
+#endif
+constexpr int kAlphaWarmBlock = TORJ_ALPHA_WARM_BLOCK;
 template <int IWARM>
-__global__ void __launch_bounds__(256, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
+__global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
     k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
     const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
-    const int i = q * 256 + threadIdx.x;
+    const int i = q * kAlphaWarmBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
     const int ti = sp.tinfo[i];
@@ -2773,7 +2777,6 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                  b_awork = a.counters ? al(4 * sizeof(unsigned) * n * kb) : 0,
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
-    const int nq = (int)((n + 255) / 256);
     // the streamed deposition's per-ray walk state (fa: the reference profile;
     // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
     // TORJ_DEPO_STREAM=1: the windows on the scan's stream, after each scan;
@@ -2909,13 +2912,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             TORJ_SPLIT_DISPATCH(k_traj, dim3(G), dim3(64), 0, sT, a, sp);
         HIPCK(hipEventRecord(p->ev_T[r], sT));
         HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
-        const dim3 agrid((unsigned)(nq * 4 * sp.kb));
         const int nqA = (int)((n + kAlphaBlock - 1) / kAlphaBlock);
         const dim3 agridA((unsigned)(nqA * 4 * sp.kb));
+        const int nqW = (int)((n + kAlphaWarmBlock - 1) / kAlphaWarmBlock);
+        const dim3 agridW((unsigned)(nqW * 4 * sp.kb));
         if (a.abs_model == 3)
-            hipLaunchKernelGGL(k_alpha_warm_pts<3>, agrid, dim3(256), 0, s2, a, sp, nq);
+            hipLaunchKernelGGL(k_alpha_warm_pts<3>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
         else if (a.abs_model == 2)
-            hipLaunchKernelGGL(k_alpha_warm_pts<1>, agrid, dim3(256), 0, s2, a, sp, nq);
+            hipLaunchKernelGGL(k_alpha_warm_pts<1>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
         else if (sp.awork)  // a counted launch
             hipLaunchKernelGGL(k_alpha_pts<true>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         else
