@@ -1304,7 +1304,7 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 #define TORJ_WARM3_ALPHA_WAVES 1
 #endif
 #ifndef TORJ_ALPHA_WARM_BLOCK
-#define TORJ_ALPHA_WARM_BLOCK 256  // lanes per warm-alpha workgroup
+#define TORJ_ALPHA_WARM_BLOCK 128  // lanes per warm-alpha workgroup (C5: 143.3 ms against 149.0 at 256)
 #endif
 constexpr int kAlphaWarmBlock = TORJ_ALPHA_WARM_BLOCK;
 template <int IWARM>
