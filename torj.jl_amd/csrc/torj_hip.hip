@@ -1304,7 +1304,8 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 #define TORJ_WARM3_ALPHA_WAVES 1
 #endif
 #ifndef TORJ_ALPHA_WARM_BLOCK
-#define TORJ_ALPHA_WARM_BLOCK 128  // lanes per warm-alpha workgroup (C5: 143.3 ms against 149.0 at 256)
+#define TORJ_ALPHA_WARM_BLOCK 64  // lanes per warm-alpha workgroup (C5: 139.3 ms against 142.6-143.2
+// at 128 and 149.0 at 256, alternating)
 #endif
 constexpr int kAlphaWarmBlock = TORJ_ALPHA_WARM_BLOCK;
 template <int IWARM>
