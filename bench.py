@@ -289,7 +289,7 @@ def main():
                  else f"k_trace_sched<{at}, {dm}, true, {int(adaptive)}>" if sched
                  else f"k_trace<{at}, {dm}, true, 16>" if lpr16
                  else f"k_trace<{at}, {dm}, true>")  # rocprof's name of the instance
-        traffic = measured_traffic(kname, n, args)
+        traffic = measured_traffic(kname, n, args, L.torj_build_id().decode())
         kern_s = float(km[0].item()) / 1e3
         flop_source = ("algorithmic (torj_hip/flops.py algorithmic_flops_warm x the kernel's "
                        "8 work counters; a lower bound, oracle/flopcount_warm.py)"
@@ -328,6 +328,8 @@ def main():
                 "n_psi": args.n_psi,
                 "traj_stride": args.traj_stride,
                 "absorption": args.absorption,
+                "build_id": L.torj_build_id().decode(),
+                "torj_env": torj_env(),
                 "parallelism": (f"ray-shard x{world} on ONE device (TORJ_BENCH_SAME_DEVICE rehearsal, "
                                 f"gloo all_reduce of dP/dV)" if same_dev
                                 else f"ray-shard x{world} + RCCL all_reduce of dP/dV"),
@@ -783,12 +785,21 @@ def entry_timing(T, plasma, pos, dirs, omega, mode, t_first):
             "host_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())}
 
 
-def measured_traffic(kname, n, args):
+def torj_env():
+    """The TORJ_* switches of this process (kernel variants, schedules): a
+    profile is paired only with a run under the same switches."""
+    return {k: v for k, v in sorted(os.environ.items())
+            if k.startswith("TORJ_") and k != "TORJ_HIP_LIB"}  # the library: its build id
+
+
+def measured_traffic(kname, n, args, build_id):
     """HBM bytes per launch of the hot kernel, measured offline by
     scripts/profile.sh (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950
     correction) and summarised by tools/prof_summary.py into
     profiles/<round>/traffic.json; used only if it was taken on this workload
-    and kernel (PMC collection cannot run inside the timed process)."""
+    and kernel, by a library of the same build id (torj_build_id(): a hash of
+    the sources and compile flags) under the same TORJ_* switches (PMC
+    collection cannot run inside the timed process)."""
     import glob
     base = kname
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*traffic.json")), reverse=True):
@@ -797,7 +808,8 @@ def measured_traffic(kname, n, args):
         except (OSError, ValueError):
             continue
         wl = t.get("workload", {})
-        if (base in (t.get("kernel") or "") and wl.get("rays") == n
+        if (wl.get("build_id") == build_id and wl.get("torj_env", {}) == torj_env()
+                and base in (t.get("kernel") or "") and wl.get("rays") == n
                 and wl.get("rk4_steps") == args.n_steps and wl.get("n_psi") == args.n_psi
                 and wl.get("traj_stride") == args.traj_stride
                 and wl.get("absorption", "albajar") == args.absorption):

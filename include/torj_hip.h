@@ -34,9 +34,10 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 6  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
+#define TORJ_ABI_VERSION 7  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
                                5: torj_trace_beam_device, torj_power_deposition_profile;
-                               6: torj_beam_timing_read, torj_trace_beam's automatic shards */
+                               6: torj_beam_timing_read, torj_trace_beam's automatic shards;
+                               7: torj_build_id */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -53,6 +54,10 @@ typedef struct torj_plasma_s *torj_plasma_t;
 
 /* ---- library / device ---------------------------------------------------- */
 int torj_abi_version(void);
+/* identity of this build: 16 hex digits of a hash over the library's sources
+ * and compile flags (csrc/Makefile).  Profiles record it, and bench.py uses a
+ * committed profile only when its build id equals the loaded library's. */
+const char *torj_build_id(void);
 const char *torj_last_error(void);
 int torj_device_count(int *n);
 

@@ -20,6 +20,5 @@ for spec in specs:
     open(p, "w").write(s.replace(a, b))
 out = os.path.join(ROOT, "torj.jl_amd", "build", "variants", f"libtorj_hip_{name}.so")
 os.makedirs(os.path.dirname(out), exist_ok=True)
-subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC",
-                       "-fopenmp", "-shared", "-o", out, "torj_hip.hip", "-L/opt/rocm/lib", "-lrccl"], cwd=f"{base}/pkg/csrc")
+subprocess.check_call(["make", "-s", "-C", f"{base}/pkg/csrc", f"LIB={out}"])
 print(out)

@@ -28,7 +28,9 @@ def test_library_exports_every_declared_symbol(T):
 
 
 def test_abi_version_and_errors(T):
-    assert T.lib().torj_abi_version() == T._lib.ABI_VERSION == 6
+    assert T.lib().torj_abi_version() == T._lib.ABI_VERSION == 7
+    bid = T.lib().torj_build_id().decode()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid), bid
     with pytest.raises(ValueError, match="N_rings"):
         T.launch_peripheral_rays([0, 0, 0], [0, 0, 1.0], 0.0174, 1 / 3.99, 92.5e9, N_rings=1)
     with pytest.raises(T.TorjError, match="abs_Al_init"):

@@ -34,6 +34,7 @@ def workload(src):
                 return {"rays": c["rays_per_gpu"], "rk4_steps": c["rk4_steps"],
                         "n_psi": c.get("n_psi"), "traj_stride": c.get("traj_stride"),
                         "absorption": c.get("absorption", "albajar"),
+                        "build_id": c.get("build_id"), "torj_env": c.get("torj_env", {}),
                         "kernel_ms_bench": d["roofline"]["kernel_ms"]}
     except (OSError, ValueError, KeyError):
         pass

@@ -2275,6 +2275,11 @@ extern "C" {
 
 int torj_abi_version(void) { return TORJ_ABI_VERSION; }
 
+#ifndef TORJ_BUILD_ID
+#define TORJ_BUILD_ID "unstamped"
+#endif
+const char *torj_build_id(void) { return TORJ_BUILD_ID; }
+
 const char *torj_last_error(void) { return g_err.c_str(); }
 
 int torj_device_count(int *n) {

@@ -52,6 +52,7 @@ class BeamShard(C.Structure):
 
 _SIGS = {
     "torj_abi_version": (C.c_int, []),
+    "torj_build_id": (C.c_char_p, []),
     "torj_last_error": (C.c_char_p, []),
     "torj_device_count": (C.c_int, [_ip]),
     "torj_abs_al_init": (C.c_int, [C.c_int]),
@@ -106,7 +107,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 6  # include/torj_hip.h TORJ_ABI_VERSION
+ABI_VERSION = 7  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 
