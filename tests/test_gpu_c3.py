@@ -77,7 +77,7 @@ def test_c3_fan_reference_deposition_vs_fitpack(c3, oplasma):
         assert abs(g.P_dep[i] - P) <= 1e-11 * max(P, 1e-300), (i, g.P_dep[i], P)
 
 
-def _close(a, b, tol):
+def _close(a, b, tol, tau_floor=1e-13):
     """Per-ray outputs equal to rounding: the split path's kernels are compiled
     separately from the fused one, so fma contraction may differ (~1e-15 on x, N;
     tau to tol relative, 1e-14 absolute)."""
@@ -94,7 +94,9 @@ def _close(a, b, tol):
     # trajectory kernel evaluates the fields in per-cell power form (the same
     # interpolant, other roundings: x, N within ~4e-16), which moves tau of a
     # weakly absorbed ray by up to ~3e-14 against the fused kernels' stencil
-    assert (np.abs(sa[:, 6] - sb[:, 6]) - tol * np.abs(sa[:, 6])).max() <= 1e-13
+    # (the node-stencil trajectory modes keep the round-3 floor of 1e-14:
+    # tests/test_gpu_split.py test_node_stencil_modes_keep_round3_bars)
+    assert (np.abs(sa[:, 6] - sb[:, 6]) - tol * np.abs(sa[:, 6])).max() <= tau_floor
     # the reference deposition locates each shell-boundary root of the psi(s)
     # spline; where a ray grazes a boundary (near-double root) an ulp of
     # trajectory moves the root by ~sqrt(eps), or makes a tangency a root pair

@@ -353,6 +353,59 @@ def _env_run(T, hplasma, env, *args, **kw):
                 os.environ[k] = v
 
 
+@pytest.mark.parametrize("mode", ["0", "1", "2"])
+def test_node_stencil_modes_keep_round3_bars(gpu, T, hplasma, mode):
+    """The widened bars of the split path (tau floor 1e-13 against the fused
+    kernel, warm model 2 tau 1e-9) belong to the cell power form only
+    (TORJ_TRAJ_LDS=3, the default): with a node-stencil trajectory kernel
+    (0: L2, 1: whole-grid LDS, 2: node tile) -- the fused kernels' arithmetic --
+    the split path holds the round-3 bars: x, N 1e-12, tau 1e-12 relative with
+    a 1e-14 floor, and warm model 2 tau 1e-10 relative."""
+    from test_gpu_c3 import _close
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, psi_grid=np.linspace(0, 1, 1000),
+              deposition="reference", x_launch=pos, s0=s0)
+    a = _run(T, hplasma, 0, 0, xp, Np, om, 1, **kw)
+    b = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, **kw)
+    _close(a, b, 1e-12, tau_floor=1e-14)
+    kw.update(absorption=2, psi_grid=np.linspace(0, 1, 500))
+    a = _run(T, hplasma, 1, 0, xp, Np, om, 1, **kw)
+    b = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, **kw)
+    assert np.array_equal(a.status, b.status) and np.array_equal(a.steps, b.steps)
+    assert a.state[:, 6].min() > 1.0  # the X2 layer is crossed
+    e = (np.abs(a.state[:, 6] - b.state[:, 6]) / a.state[:, 6]).max()
+    assert e <= 1e-10, e
+    print(f"TORJ_TRAJ_LDS={mode}: warm model 2 split vs fused tau {e:.1e}")
+
+
+@pytest.mark.parametrize("mode", ["0", "1", "2", "3"])
+def test_nan_alpha_replay_bit_identical(gpu, T, hplasma, mode):
+    """A ray whose alpha goes non-finite at step s stops NAN with the state
+    x_s, which k_split_final rebuilds from the chunk-boundary copy by replaying
+    the steps since (cold_replay).  The replay uses the arithmetic of the
+    trajectory kernel that ran (cell power form for TORJ_TRAJ_LDS=3, the node
+    stencil otherwise), so x_s is bit for bit the trajectory's own: the test
+    hook TORJ_TEST_NAN_ALPHA_STEP=s makes the scan read alpha as NaN at step s
+    for every third ray, and those rays must equal a clean trace of s steps."""
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    s_nan = 537  # mid-chunk (chunk 20): a replay of 17 steps
+    kw = dict(ds=1e-4, weights=w, traj_stride=0, chunk_steps=20)
+    clean_full = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, n_steps=1500, **kw)
+    hooked = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode, "TORJ_TEST_NAN_ALPHA_STEP": str(s_nan)},
+                      xp, Np, om, 1, n_steps=1500, **kw)
+    clean_s = _env_run(T, hplasma, {"TORJ_TRAJ_LDS": mode}, xp, Np, om, 1, n_steps=s_nan, **kw)
+    idx = np.arange(len(w))
+    hit = (idx % 3 == 0) & (clean_s.status == T.OK) & (clean_s.steps == s_nan)
+    assert hit.sum() > 50
+    assert (hooked.status[hit] == T.NAN).all() and (hooked.steps[hit] == s_nan).all()
+    assert np.array_equal(hooked.state[hit, :6], clean_s.state[hit, :6])
+    rest = ~hit & ((idx % 3 != 0) | (clean_s.status != T.OK))
+    for f in ("status", "steps"):
+        assert np.array_equal(getattr(hooked, f)[rest], getattr(clean_full, f)[rest]), f
+    assert np.array_equal(hooked.state[rest], clean_full.state[rest])
+
+
 @pytest.mark.parametrize("tile,caps", [("2", ("30", "0")), ("3", ("2", "0"))])
 def test_traj_tile_bit_identical_to_global_fallback(gpu, T, hplasma, tile, caps):
     """k_traj_tile (TORJ_TRAJ_LDS=2) stages per wave only the coefficient tile

@@ -901,6 +901,9 @@ struct SplitArgs {
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
     int tile_cap;         // k_traj_tile: most nodes a wave stages (<= kTileNodes)
     double tile_margin;   // k_traj_tile: the box's margin in units of the block's path, (kb + 1) ds
+    int cell;             // the trajectory kernel is k_traj_cell: the NaN-alpha replay uses its arithmetic
+    int nan_step;         // test hook (TORJ_TEST_NAN_ALPHA_STEP, default -1): the scan reads alpha as NaN
+                          // at this step for every third ray, to exercise the NaN-alpha replay
 };
 
 // steps | status << 24: split launches need n_steps < kSplitMaxSteps (the
@@ -1249,8 +1252,9 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArg
     traj_body<DEPO, TRAJ, kTrajCell>(a, sp);
 }
 
-// alpha at the stored stage points of one block: block = 256 lanes = 4 groups
-// of 64 rays at one (step j, stage); lanes of rays the trajectory did not
+// alpha at the stored stage points of one block: block = kAlphaBlock lanes
+// (TORJ_ALPHA_BLOCK, default 128: two groups of 64 rays) at one (step j,
+// stage); lanes of rays the trajectory did not
 // reach this step with (or the scan has stopped) sit out, as in the fused wave
 // (a measured alternative -- harmonic 2 in a second pass over a compacted list
 // of the points needing it -- executed more instructions in total: the points
@@ -1327,12 +1331,19 @@ __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA
                                      ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
 }
 
-// RK4 ray_segment from x, N over `k` steps without stores (the NaN-alpha replay)
-__device__ void cold_replay(const TraceArgs &a, double x[3], double N[3], int k) {
+// RK4 ray_segment from x, N over `k` steps without stores (the NaN-alpha
+// replay), in the arithmetic of the trajectory kernel that ran: the cell power
+// form from the global cell table after k_traj_cell (bit for bit its steps:
+// a tile and the global table give the same bits), the node stencil otherwise
+__device__ void cold_replay(const TraceArgs &a, const SplitArgs &sp, double x[3], double N[3], int k) {
     SplitArgs none{};
+    const TileCell cg{a.cellp, nullptr, 0, 0, 0, 0};
     for (int s = 0; s < k; s++) {
         double xn[3], Nn[3];
-        cold_step<false>(a, a.coef, none, 0, 0, x, N, xn, Nn);
+        if (sp.cell)
+            cold_step<false, kTileNS, TileCell>(a, cg, none, 0, 0, x, N, xn, Nn);
+        else
+            cold_step<false>(a, a.coef, none, 0, 0, x, N, xn, Nn);
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             x[c] = xn[c];
@@ -1392,7 +1403,8 @@ __device__ __forceinline__ void tau_scan_body(const TraceArgs &a, const SplitArg
                         break;
                     }
                     const size_t o = (size_t)(s - sp.k0) * 4 * a.n + i;
-                    const double al0 = alb[v][0], al1 = alb[v][1], al2 = alb[v][2], al3 = alb[v][3];
+                    const double al0 = (s == sp.nan_step && i % 3 == 0) ? (double)NAN : alb[v][0];
+                    const double al1 = alb[v][1], al2 = alb[v][2], al3 = alb[v][3];
                     double acc_a = fma(1.0, al0, 0.0);
                     acc_a = fma(2.0, al1, acc_a);
                     acc_a = fma(2.0, al2, acc_a);
@@ -1509,7 +1521,7 @@ __global__ void __launch_bounds__(64) k_split_final(TraceArgs a, SplitArgs sp) {
             x[c] = cb[c * (size_t)a.n];
             N[c] = cb[(3 + c) * (size_t)a.n];
         }
-        cold_replay(a, x, N, steps - c0 * (a.chunk_steps > 0 ? cs : 0));
+        cold_replay(a, sp, x, N, steps - c0 * (a.chunk_steps > 0 ? cs : 0));
         if constexpr (TRAJ) {  // samples the trajectory wrote past the stop
             if (a.traj_stride > 0)
                 for (int k = steps / a.traj_stride; k < min(tT, a.n_steps) / a.traj_stride; k++)
@@ -1985,12 +1997,14 @@ struct torj_plasma_s {
     // single-process RCCL communicator over the first nccl_n of them
     std::vector<torj_plasma_s *> replicas;
     std::vector<ncclComm_t> comms;
-    // torj_trace_beam's host staging on this replica (beam_worker): two shard
-    // slots of device buffers and of pinned host buffers (grow-only), the copy
-    // stream and the slots' events (upload done, trace done, download done)
+    // torj_trace_beam's host staging on this replica (beam_worker): one or two
+    // shard slots of device buffers and of host buffers (grow-only; pinned up
+    // to a budget, pageable above it), the copy stream and the slots' events
+    // (upload done, trace done, download done)
     struct BeamStage {
         void *d = nullptr, *h = nullptr;
         size_t d_cap = 0, h_cap = 0;
+        bool h_pinned = false;
         hipStream_t sc = nullptr;
         hipEvent_t up[2] = {}, tr[2] = {}, dn[2] = {};
     } stage;
@@ -2377,7 +2391,12 @@ int torj_plasma_destroy(torj_plasma_t p) {
     if (p->d_coef) (void)hipSetDevice(p->device);
     if (p->stage.sc) (void)hipStreamSynchronize(p->stage.sc);
     if (p->stage.d) (void)hipFree(p->stage.d);
-    if (p->stage.h) (void)hipHostFree(p->stage.h);
+    if (p->stage.h) {
+        if (p->stage.h_pinned)
+            (void)hipHostFree(p->stage.h);
+        else
+            free(p->stage.h);
+    }
     for (int r = 0; r < 2; r++) {
         if (p->stage.up[r]) (void)hipEventDestroy(p->stage.up[r]);
         if (p->stage.tr[r]) (void)hipEventDestroy(p->stage.tr[r]);
@@ -2880,9 +2899,12 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int tile_max = lds_env == 3 ? kTileCells : kTileNodes;  // cells / nodes
     sp.tile_cap = std::min(tile_max, cap_e ? atoi(cap_e) : tile_max);
     sp.tile_margin = mar_e ? atof(mar_e) : 1.001;
+    const char *nan_e = getenv("TORJ_TEST_NAN_ALPHA_STEP");
+    sp.nan_step = nan_e ? atoi(nan_e) : -1;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
     const bool lds_traj = lds_env == 1 && lds_bytes <= 160 * 1024;
     const bool tile_traj = lds_env == 2, cell_traj = lds_env == 3;
+    sp.cell = cell_traj;
     const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
@@ -3525,14 +3547,18 @@ int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace
         return fail("n_gpus = %d, but the handle has %d replica(s)", n_gpus, std::max<int>(1, (int)p->replicas.size()));
     int dev0 = 0;
     HIPCK(hipGetDevice(&dev0));
-    for (int k = 0; k < n_gpus; k++) {
+    std::lock_guard<std::mutex> lk(p->mu);  // the replica list (torj_timing takes it too)
+    int rc = 0;
+    for (int k = 0; k < n_gpus && rc == 0; k++) {
         torj_plasma_s *q = k == 0 ? p : p->replicas[k];
-        HIPCK(hipSetDevice(q->device));
-        if (torj_timing_read(q, calls ? calls + k : nullptr, trace_ms ? trace_ms + k : nullptr,
-                             post_ms ? post_ms + k : nullptr))
-            return -1;
+        if (hipSetDevice(q->device) != hipSuccess)
+            rc = fail("hipSetDevice(%d) failed", q->device);
+        else if (torj_timing_read(q, calls ? calls + k : nullptr, trace_ms ? trace_ms + k : nullptr,
+                                  post_ms ? post_ms + k : nullptr))
+            rc = -1;
     }
-    HIPCK(hipSetDevice(dev0));
+    (void)hipSetDevice(dev0);  // the caller's device on every path
+    if (rc) return rc;
     if (reduce_ms) *reduce_ms = p->reduce_ms;
     p->reduce_ms = 0.0;
     p->reduce_calls = 0;
@@ -3763,9 +3789,13 @@ static void beam_shard(int n, int S, int k, int &lo, int &cnt) {
     cnt = (int)std::min<long>(g1 * 64, n) - lo;
 }
 
-// The staging of torj_trace_beam on replica q: device and pinned host memory
-// for two shard slots of `slot` doubles each, the copy stream and the events.
-static int beam_stage(torj_plasma_s *q, size_t slot) {
+// The staging of torj_trace_beam on replica q: device and host memory for
+// `nslots` (1 or 2) shard slots of `slot` doubles each, the copy stream and the
+// events.  The host side is pinned while it fits TORJ_BEAM_PIN_MB (default
+// 2048 MiB per replica; the transfers then run at PCIe rate and overlap the
+// trace), pageable above it (hipMemcpyAsync stages those copies itself: slower,
+// but a beam of huge user shards never fails for want of pinnable memory).
+static int beam_stage(torj_plasma_s *q, size_t slot, int nslots) {
     auto &b = q->stage;
     if (!b.sc) {
         HIPCK(hipStreamCreateWithFlags(&b.sc, hipStreamNonBlocking));
@@ -3775,18 +3805,32 @@ static int beam_stage(torj_plasma_s *q, size_t slot) {
             HIPCK(hipEventCreateWithFlags(&b.dn[r], hipEventDisableTiming));
         }
     }
-    const size_t bytes = 2 * slot * sizeof(double);
+    const size_t bytes = (size_t)nslots * slot * sizeof(double);
     if (b.d_cap < bytes) {
         if (b.d) HIPCK(hipFree(b.d));
         b.d = nullptr, b.d_cap = 0;
         HIPCK(hipMalloc(&b.d, bytes));
         b.d_cap = bytes;
     }
-    if (b.h_cap < bytes) {
-        if (b.h) HIPCK(hipHostFree(b.h));
+    const char *pin_e = getenv("TORJ_BEAM_PIN_MB");
+    const size_t pin_max = (size_t)(pin_e ? atol(pin_e) : 2048) << 20;
+    const bool pin = bytes <= pin_max;
+    if (b.h_cap < bytes || (b.h_pinned && !pin)) {
+        if (b.h) {
+            if (b.h_pinned)
+                HIPCK(hipHostFree(b.h));
+            else
+                free(b.h);
+        }
         b.h = nullptr, b.h_cap = 0;
-        HIPCK(hipHostMalloc(&b.h, bytes, hipHostMallocDefault));
+        if (pin) {
+            HIPCK(hipHostMalloc(&b.h, bytes, hipHostMallocDefault));
+        } else {
+            b.h = malloc(bytes);
+            if (!b.h) return fail("torj_trace_beam: host staging of %zu bytes failed", bytes);
+        }
         b.h_cap = bytes;
+        b.h_pinned = pin;
     }
     return 0;
 }
@@ -3833,7 +3877,8 @@ static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S
     const int n_in = 6 + (w ? 1 : 0) + (xl ? 3 : 0) + (s0 ? 1 : 0);
     const int n_out = 7 + (depo ? 1 : 0) + n_save * 5 + 1;
     const size_t slot = (size_t)(n_in + n_out) * m;
-    if (beam_stage(q, slot)) return -1;
+    const int nk = (int)los.size();
+    if (beam_stage(q, slot, nk > 1 ? 2 : 1)) return -1;  // one shard: no second slot
     auto &bs = q->stage;
     double *dbase = (double *)bs.d, *hbase = (double *)bs.h;
     struct View {  // one slot's arrays for a shard of cnt rays
@@ -3877,7 +3922,6 @@ static int beam_worker(torj_plasma_s *q, const torj_trace_cfg *cfg, int n, int S
 #pragma omp parallel for if ((size_t)rows * cnt > (1u << 18)) num_threads(8)
         for (int r = 0; r < rows; r++) memcpy(dst + (size_t)r * n + lo, src + (size_t)r * cnt, cnt * D);
     };
-    const int nk = (int)los.size();
     auto stage_in = [&](int j) -> int {  // pack shard j and queue its upload
         const int r = j & 1, lo = los[j], cnt = cnts[j];
         if (j >= 2) HIPCK(hipEventSynchronize(bs.up[r]));  // shard j - 2's upload left the slot

@@ -657,6 +657,8 @@ TORJ_HD NsPartials refractive_index_sq_partials(double X, double Y, double Npar,
     double sq = Delta * rsq;
 #ifdef __HIP_DEVICE_COMPILE__
     if (__builtin_amdgcn_class(Delta, 0x260)) sq = Delta;
+#else
+    if (Delta == 0.0 || Delta == HUGE_VAL) sq = Delta;  // the same fix-up (+-0, +inf) on the host
 #endif
     const double A = 1.0 + md * sq + Np2;
     const double Q = 2.0 * (-1.0 + X + Y2);
