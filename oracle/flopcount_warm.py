@@ -18,8 +18,9 @@ Algorithmic conventions (what is NOT counted): the factorial tables asl, bsl,
 dependent parts are counted at their cheapest branch (a lower bound):
   fsup side: alpha < 0 (no shifted arguments), large |psi| (cf32 from czp, czm);
   recursion step: the small-|psi| form (1 + phi2 cf1) / (l + 1/2);
-  warmdisp: every pass but the last of each call is a full update (the last
-  one breaks); unconverged calls (100 updates) are counted with 99.
+  warmdisp: every pass but the last of each call sums the tensor and updates
+  N_perp^2 (the last one breaks before its sum); unconverged calls (100
+  updates) are counted with 99.
 The Faddeeva value comes from scipy; its op count is that of the branch the
 kernel runs (torj_warm.hpp faddeeva_upper): the asymptotic series (10 terms)
 where |x| >= 16 or Im z >= 16, else Weideman's N = 36 complex Horner sum.  The
@@ -107,14 +108,30 @@ def cabs(a):  # hypot: x^2 + y^2 and a sqrt (scaling not counted)
     return sqrt(a.re * a.re + a.im * a.im)
 
 
-def csqrt(z):
+def cnorm(a):  # |a|^2
+    return a.re * a.re + a.im * a.im
+
+
+def csqrt(z):  # torj_warm.hpp csqrt_: |z| from the norm, one reciprocal
     if z.re.v == 0.0 and z.im.v == 0.0:
         return CC(0.0, z.im)
-    r = cabs(z)
+    r = sqrt(cnorm(z))
     t = sqrt(0.5 * (r + CF(abs(z.re.v))))
+    h = 0.5 * (1.0 / t)
     if z.re.v >= 0.0:
-        return CC(t, 0.5 * z.im / t)
-    return CC(0.5 * CF(abs(z.im.v)) / t, CF(math.copysign(t.v, z.im.v)))
+        return CC(t, z.im * h)
+    return CC(CF(abs(z.im.v)) * h, CF(math.copysign(t.v, z.im.v)))
+
+
+def root_update(cc2, sg, rr, cc4, na):
+    """warmdisp's root and convergence test as the kernel forms them: the
+    division by 2 cc4 as a product with conj(cc4) / (2 |cc4|^2), the moduli
+    from their squares (na = |anpr2a|^2, carried from the previous pass)"""
+    ic = 0.5 * (1.0 / cnorm(cc4))
+    anpr2 = (-cc2 + sg * csqrt(rr)) * CC(cc4.re * ic, -cc4.im * ic)
+    n2 = cnorm(anpr2)
+    errnpr = abs((1.0 - sqrt(n2 * (1.0 / na))).v)
+    return anpr2, n2, errnpr
 
 
 def faddeeva_weideman_count():
@@ -334,9 +351,13 @@ def alpha_wr(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode):
     anpr2a = CC(npr * npr)
     anpr2 = anpr2a
     errnpr = 1.0
+    na = cnorm(anpr2a)
     tr.converged = False
     for i in range(1, 101):
         tr.passes = i
+        if i > 2 and errnpr < 1e-4:  # before the sum: alpha needs no polarisation
+            tr.converged = True
+            break
         s = [CC(0.0)] * 6
         pwc = CC(1.0)
         for l in range(lrm):
@@ -345,9 +366,6 @@ def alpha_wr(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode):
             pwc = pwc * anpr2a
         e11, e12, e22, a13, a23, a33 = s
         a31, a32 = a13, -a23
-        if i > 2 and errnpr < 1e-4:
-            tr.converged = True
-            break
         em, ep = e11 - anpl2, e22 - anpl2
         oa = 1.0 - a33
         a13p, a31p = a13 + anpl, a31 + anpl
@@ -362,8 +380,7 @@ def alpha_wr(omega, X, Y, N_abs, N_par, Te, inv_dDdN, mode):
             sg = float(-sox)
             if rr.re.v <= 0.0 and rr.im.v >= 0.0:
                 sg = -sg
-        anpr2 = (-cc2 + sg * csqrt(rr)) / (2.0 * cc4)
-        errnpr = abs((1.0 - cabs(anpr2) / cabs(anpr2a)).v)
+        anpr2, na, errnpr = root_update(cc2, sg, rr, cc4, na)
         anpr2a = anpr2
     if anpr2.re.v < 0.0 and anpr2.im.v < 0.0:
         anpr2 = CC(0.0)
@@ -444,7 +461,7 @@ def _update_count():
     """one warmdisp update (cc4, cc2, cc0, discriminant, root, convergence test)"""
     e = [CC(0.1 * (q + 1), 0.05 * q) for q in range(6)]
     e330, anpl, anpl2 = CC(0.9, 0.01), CF(0.2), CF(0.04)
-    anpr2a = CC(0.5, 0.01)
+    na = CF(0.25)
 
     def upd():
         e11, e12, e22, a13, a23, a33 = e
@@ -457,8 +474,7 @@ def _update_count():
                - (a23 * a32 + e330 + ep * oa) * em - a13p * a31p * ep)
         cc0 = e330 * (em * ep + e12 * e12)
         rr = cc2 * cc2 - 4.0 * cc0 * cc4
-        anpr2 = (-cc2 + 1.0 * csqrt(rr)) / (2.0 * cc4)
-        _ = 1.0 - cabs(anpr2) / cabs(anpr2a)
+        _ = root_update(cc2, 1.0, rr, cc4, na)
     return _n(upd)
 
 
@@ -487,7 +503,8 @@ def _call_count():
         cq2p0 = p0[1] + amu_anpl2[1] * (p0[2] + p0[0] - 2.0 * p0[1])
         _ = 1.0 - (X * mu) * cq2p0
         _ = e0[0] + 1.0, e0[2] + 1.0
-        _ = CC(npr * npr)
+        a = CC(npr * npr)
+        _ = cnorm(a)  # |anpr2a|^2 of the first pass
         _ = 2.0 * CF(0.1) * CF(1e11) / KC * CF(0.5)
     return _n(call)
 
@@ -505,7 +522,7 @@ def model_flops(tr_list, c):
                 + tr.nasym * c["FLOPS_WARM_FADDEEVA_ASYM"] + (2 * L + 1) * c["FLOPS_WARM_SIDE"]
                 + steps * c["FLOPS_WARM_STEP"] + stored * c["FLOPS_WARM_STORE"]
                 + (L + 1) * c["FLOPS_WARM_ISA"] + (L * L + 3 * L) // 2 * c["FLOPS_WARM_PAIR"]
-                + L * c["FLOPS_WARM_ORDER"] + tr.passes * L * c["FLOPS_WARM_SUM_TERM"]
+                + L * c["FLOPS_WARM_ORDER"] + upd * L * c["FLOPS_WARM_SUM_TERM"]
                 + upd * c["FLOPS_WARM_UPDATE"])
     return tot
 

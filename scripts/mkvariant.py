@@ -1,13 +1,16 @@
 """Build an A/B variant of libtorj_hip.so from a patched copy of the sources
-(profiling aid, never shipped): python scripts/mkvariant.py NAME 'file|||old|||new' ...
--> torj.jl_amd/build/variants/libtorj_hip_NAME.so (run by scripts/gpu_ab.sh)."""
+(profiling aid, never shipped): python scripts/mkvariant.py NAME [-DFLAG ...] 'file|||old|||new' ...
+-> torj.jl_amd/build/variants/libtorj_hip_NAME.so (run by scripts/gpu_ab.sh); -D... arguments are
+extra compile flags (e.g. -DTORJ_WARM_PROF, the warm alpha's region timers: tools/warm_prof.py)."""
 import os
 import shutil
 import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-name, specs = sys.argv[1], sys.argv[2:]
+name = sys.argv[1]
+flags = [a for a in sys.argv[2:] if a.startswith("-D")]
+specs = [a for a in sys.argv[2:] if not a.startswith("-D")]
 base = f"/tmp/torj_variant/{name}"
 shutil.rmtree(base, ignore_errors=True)
 shutil.copytree(os.path.join(ROOT, "torj.jl_amd", "csrc"), f"{base}/pkg/csrc")
@@ -20,5 +23,5 @@ for spec in specs:
     open(p, "w").write(s.replace(a, b))
 out = os.path.join(ROOT, "torj.jl_amd", "build", "variants", f"libtorj_hip_{name}.so")
 os.makedirs(os.path.dirname(out), exist_ok=True)
-subprocess.check_call(["make", "-s", "-C", f"{base}/pkg/csrc", f"LIB={out}"])
+subprocess.check_call(["make", "-s", "-C", f"{base}/pkg/csrc", f"LIB={out}", "EXTRA=" + " ".join(flags)])
 print(out)

@@ -901,9 +901,13 @@ struct SplitArgs {
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
     int tile_cap;         // k_traj_tile: most nodes a wave stages (<= kTileNodes)
     double tile_margin;   // k_traj_tile: the box's margin in units of the block's path, (kb + 1) ds
-    int cell;             // the trajectory kernel is k_traj_cell: the NaN-alpha replay uses its arithmetic
+    int traj_mode;        // the trajectory kernel (kTrajL2 .. kTrajCell): the NaN-alpha replay uses its arithmetic
     int nan_step;         // test hook (TORJ_TEST_NAN_ALPHA_STEP, default -1): the scan reads alpha as NaN
                           // at this step for every third ray, to exercise the NaN-alpha replay
+    unsigned long long *defer;  // warm: the block's points with lrm > 3, (js << 32) | i, for k_alpha_warm_big
+    unsigned *defer_cnt;        // warm: their count (this block's slot, zeroed per launch)
+    int defer_lrm;              // warm: points with lrm above this are deferred (3; TORJ_WARM_DEFER_LRM
+                                // lowers it: a test sends every point through the deferred path)
 };
 
 // steps | status << 24: split launches need n_steps < kSplitMaxSteps (the
@@ -1275,23 +1279,28 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     const int i = q * kAlphaBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
-    const int ti = sp.tinfo[i];
+    // every load of the point at once (one memory latency, not three in a
+    // row): the stop words and the inputs, whose addresses are valid for any
+    // i < n whether or not the point is live
+    const int ti = sp.tinfo[i], si = sp.sinfo[i];
+    const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
+    const double X = in[0], Y = in[(size_t)a.n], N2 = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
+    const double lnTe = in[4 * (size_t)a.n];
     // sinfo may be stale (k_tau_scan of an earlier block runs on another
     // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
     // alpha the scan never reads
-    if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
-    const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
-    const double Nabs = sqrt_pos(in[2 * (size_t)a.n]), Te = exp_fast(in[4 * (size_t)a.n]);
+    if (sp.k0 + j >= info_steps(ti) || info_status(si) != ST_OK) return;
+    const double Nabs = sqrt_pos(N2), Te = exp_fast(lnTe);
     if constexpr (COUNT) {
         AlbajarWork work = {};
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, in[0], in[(size_t)a.n], Nabs, in[3 * (size_t)a.n], Te, a.mode, &work);
+            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, &work);
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
                                      ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
     } else {
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, in[0], in[(size_t)a.n], Nabs, in[3 * (size_t)a.n], Te, a.mode, nullptr);
+            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, nullptr);
     }
 }
 
@@ -1312,6 +1321,12 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 // at 128 and 149.0 at 256, alternating)
 #endif
 constexpr int kAlphaWarmBlock = TORJ_ALPHA_WARM_BLOCK;
+__device__ __forceinline__ void warm_store(const SplitArgs &sp, int js, int i, int n, const WarmAlpha &r) {
+    sp.alpha[(size_t)js * n + i] = r.alpha;
+    if (sp.awork)
+        sp.awork[(size_t)js * n + i] = (unsigned)min(r.nasym, 127) | ((unsigned)min(r.nfad, 127) << 7) |
+                                   ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
+}
 template <int IWARM>
 __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
     k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
@@ -1319,31 +1334,81 @@ __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA
     const int i = q * kAlphaWarmBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
-    const int ti = sp.tinfo[i];
-    if (sp.k0 + j >= info_steps(ti) || info_status(sp.sinfo[i]) != ST_OK) return;
+    // every load of the point at once (as k_alpha_pts)
+    const int ti = sp.tinfo[i], si = sp.sinfo[i];
     const double *in = sp.ain + (size_t)js * kAinFW * a.n + i;
-    const WarmAlpha r = alpha_warm_v<IWARM>(a.omega, in[0], in[(size_t)a.n], in[2 * (size_t)a.n],
-                                            in[3 * (size_t)a.n], in[4 * (size_t)a.n],
-                                            in[5 * (size_t)a.n], a.mode);
-    sp.alpha[(size_t)js * a.n + i] = r.alpha;
-    if (sp.awork)
-        sp.awork[(size_t)js * a.n + i] = (unsigned)min(r.nasym, 127) | ((unsigned)min(r.nfad, 127) << 7) |
-                                     ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
+    const double X = in[0], Y = in[(size_t)a.n], Nabs = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
+    const double Te = in[4 * (size_t)a.n], inv = in[5 * (size_t)a.n];
+    if (sp.k0 + j >= info_steps(ti) || info_status(si) != ST_OK) return;
+#if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    static_assert(kAlphaWarmBlock == 64, "region timers: one wave per workgroup");
+    wprof_init();
+#endif
+    const WarmSetup w = warm_setup(Y, Nabs, Npar, Te);
+    // a point with lrm > 3 (~0.1 % of the C5 beam's) goes to k_alpha_warm_big:
+    // this kernel then holds the lrm <= 3 tensor only (its registers, and so
+    // the waves per SIMD, are sized for that), and no wave runs the lrm <= 5
+    // code for all its lanes because one of them needs it
+    const bool big = w.lrm > sp.defer_lrm;
+    const unsigned long long bmask = __ballot(big);
+    if (bmask) {  // wave-aggregated append
+        const int lane = (int)__lane_id(), lead = __builtin_ffsll((long long)bmask) - 1;
+        unsigned base = 0;
+        if (lane == lead) base = atomicAdd(sp.defer_cnt, (unsigned)__popcll(bmask));
+        base = __shfl(base, lead);
+        if (big)
+            sp.defer[base + __popcll(bmask & ((1ull << lane) - 1))] =
+                ((unsigned long long)js << 32) | (unsigned)i;
+    }
+    if (big) return;
+    const WarmAlpha r = alpha_warm_l<IWARM, 3>(a.omega, X, Y, Npar, w, inv, a.mode);
+    warm_store(sp, js, i, a.n, r);
+#if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    TORJ_WPROF(6);  // the stores
+    wprof_flush();
+#endif
 }
 
-// RK4 ray_segment from x, N over `k` steps without stores (the NaN-alpha
-// replay), in the arithmetic of the trajectory kernel that ran: the cell power
-// form from the global cell table after k_traj_cell (bit for bit its steps:
-// a tile and the global table give the same bits), the node stencil otherwise
-__device__ void cold_replay(const TraceArgs &a, const SplitArgs &sp, double x[3], double N[3], int k) {
-    SplitArgs none{};
+// the points k_alpha_warm_pts deferred (lrm > 3), with the lrm <= 5 tensor;
+// after it on the same stream, a fixed grid striding over the block's list
+#ifndef TORJ_WARM_BIG_GRID
+#define TORJ_WARM_BIG_GRID 512  // workgroups of 64: two waves per CU
+#endif
+template <int IWARM>
+__global__ void __launch_bounds__(64) k_alpha_warm_big(TraceArgs a, SplitArgs sp) {
+    const unsigned cnt = *sp.defer_cnt;
+    for (unsigned k = blockIdx.x * 64 + threadIdx.x; k < cnt; k += gridDim.x * 64) {
+        const unsigned long long e = sp.defer[k];
+        const int js = (int)(e >> 32), i = (int)(unsigned)e;
+        const double *in = sp.ain + (size_t)js * kAinFW * a.n + i;
+        const double Npar = in[3 * (size_t)a.n];
+        const WarmSetup w = warm_setup(in[(size_t)a.n], in[2 * (size_t)a.n], Npar, in[4 * (size_t)a.n]);
+        const WarmAlpha r = alpha_warm_l<IWARM, kWarmMaxL>(a.omega, in[0], in[(size_t)a.n], Npar, w,
+                                                            in[5 * (size_t)a.n], a.mode);
+        warm_store(sp, js, i, a.n, r);
+    }
+}
+
+// RK4 ray_segment from x, N over `k` steps (the NaN-alpha replay) in the
+// arithmetic of the trajectory kernel that ran (sp.traj_mode): the same
+// cold_step instance -- its stage-0 stencil with psi and its alpha-input
+// stores, which change the compiler's fma contraction, here into row j = 0 of
+// the ring slot sp.ain (no alpha kernel reads it any more: k_split_final runs
+// after the last scan) -- read from the global table its tile falls back to
+// (bit for bit the tile's values): the cell power form after k_traj_cell, the
+// node tile's fallback after k_traj_tile, the node stencil otherwise (k_traj;
+// k_traj_lds reads the same values from LDS, in a separately compiled kernel)
+__device__ void cold_replay(const TraceArgs &a, const SplitArgs &sp, int i, double x[3], double N[3], int k) {
     const TileCell cg{a.cellp, nullptr, 0, 0, 0, 0};
+    const TileCoef ng{a.coef, nullptr, 0, 0, 0, 0};
     for (int s = 0; s < k; s++) {
-        double xn[3], Nn[3];
-        if (sp.cell)
-            cold_step<false, kTileNS, TileCell>(a, cg, none, 0, 0, x, N, xn, Nn);
+        double xn[3], Nn[3], psi;
+        if (sp.traj_mode == kTrajCell)
+            cold_step<true, kTileNS, TileCell, true>(a, cg, sp, 0, i, x, N, xn, Nn, &psi);
+        else if (sp.traj_mode == kTrajTile)
+            cold_step<true, kTileNS, TileCoef, true>(a, ng, sp, 0, i, x, N, xn, Nn, &psi);
         else
-            cold_step<false>(a, a.coef, none, 0, 0, x, N, xn, Nn);
+            cold_step<true, kNF, const double *, true>(a, a.coef, sp, 0, i, x, N, xn, Nn, &psi);
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             x[c] = xn[c];
@@ -1521,7 +1586,7 @@ __global__ void __launch_bounds__(64) k_split_final(TraceArgs a, SplitArgs sp) {
             x[c] = cb[c * (size_t)a.n];
             N[c] = cb[(3 + c) * (size_t)a.n];
         }
-        cold_replay(a, sp, x, N, steps - c0 * (a.chunk_steps > 0 ? cs : 0));
+        cold_replay(a, sp, i, x, N, steps - c0 * (a.chunk_steps > 0 ? cs : 0));
         if constexpr (TRAJ) {  // samples the trajectory wrote past the stop
             if (a.traj_stride > 0)
                 for (int k = steps / a.traj_stride; k < min(tT, a.n_steps) / a.traj_stride; k++)
@@ -2294,6 +2359,18 @@ int torj_abi_version(void) { return TORJ_ABI_VERSION; }
 #endif
 const char *torj_build_id(void) { return TORJ_BUILD_ID; }
 
+#ifdef TORJ_WARM_PROF
+// profiling build only (not in include/torj_hip.h): the warm alpha's region
+// timers -- out[0] waves, out[1 + k] clock ticks of region k -- read and reset
+int torj_warm_prof_read(unsigned long long *out) {
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wprof), sizeof(g_wprof)));
+    static const unsigned long long zero[kWProfN + 1] = {};
+    HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), zero, sizeof(g_wprof)));
+    return 0;
+}
+#endif
+
 const char *torj_last_error(void) { return g_err.c_str(); }
 
 int torj_device_count(int *n) {
@@ -2814,8 +2891,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const bool dstream = fa && dso && dstream_env != 0;
     const size_t b_dsd = dstream ? al(kDsNd * sizeof(double) * n) : 0,
                  b_dsi = dstream ? al(kDsNi * sizeof(int) * n) : 0;
+    // warm: the list of deferred (lrm > 3) points of a block (one list: the
+    // alpha kernels of consecutive blocks are ordered on one stream) and one
+    // counter per block
+    const int n_blk = (int)((n_steps + kb - 1) / kb);
+    const size_t b_defer = a.abs_model >= 2 ? al(4 * sizeof(unsigned long long) * n * kb) : 0,
+                 b_dcnt = a.abs_model >= 2 ? al(sizeof(unsigned) * n_blk) : 0;
     const size_t bytes = R * (b_ain + b_alpha + b_awork) + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
-                         2 * b_n4 + b_dsd + b_dsi;
+                         2 * b_n4 + b_dsd + b_dsi + b_defer + b_dcnt;
     if (ensure_split(p, bytes)) return -1;
     char *q = (char *)p->d_split;
     auto take = [&](size_t b) {
@@ -2843,6 +2926,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     sp.sPdep = (double *)take(b_n8);
     sp.tinfo = (int *)take(b_n4);
     sp.sinfo = (int *)take(b_n4);
+    unsigned long long *defer = b_defer ? (unsigned long long *)take(b_defer) : nullptr;
+    unsigned *dcnt = b_dcnt ? (unsigned *)take(b_dcnt) : nullptr;
+    sp.defer = defer;
     DepoStream ds{};
     if (dstream) {
         ds.d = (double *)take(b_dsd);
@@ -2882,6 +2968,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     HIPCK(hipMemsetAsync(sp.stau, 0, 3 * b_n8, sT));
     HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, sT));
     if (dstream) HIPCK(hipMemsetAsync(ds.v + kDsJ * n, 0xFF, n * sizeof(int), sT));  // j = -1: not started
+    if (dcnt) HIPCK(hipMemsetAsync(dcnt, 0, n_blk * sizeof(unsigned), s2));  // the alpha kernels' stream
     const size_t fit_lds = fa && fa->n_psi <= kFitGridLds ? (size_t)fa->n_psi * sizeof(double) : 0;
     const int G = (int)((n + 63) / 64);
     // the trajectory kernel with the coefficients staged in LDS whenever the grid
@@ -2901,10 +2988,12 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     sp.tile_margin = mar_e ? atof(mar_e) : 1.001;
     const char *nan_e = getenv("TORJ_TEST_NAN_ALPHA_STEP");
     sp.nan_step = nan_e ? atoi(nan_e) : -1;
+    const char *dl_e = getenv("TORJ_WARM_DEFER_LRM");
+    sp.defer_lrm = dl_e ? std::min(3, std::max(0, atoi(dl_e))) : 3;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
     const bool lds_traj = lds_env == 1 && lds_bytes <= 160 * 1024;
     const bool tile_traj = lds_env == 2, cell_traj = lds_env == 3;
-    sp.cell = cell_traj;
+    sp.traj_mode = cell_traj ? kTrajCell : tile_traj ? kTrajTile : lds_traj ? kTrajLds : kTrajL2;
     const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
     const int n_blocks = (int)((n_steps + kb - 1) / kb);
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
@@ -2944,10 +3033,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const dim3 agridA((unsigned)(nqA * 4 * sp.kb));
         const int nqW = (int)((n + kAlphaWarmBlock - 1) / kAlphaWarmBlock);
         const dim3 agridW((unsigned)(nqW * 4 * sp.kb));
-        if (a.abs_model == 3)
+        sp.defer_cnt = dcnt ? dcnt + b : nullptr;
+        if (a.abs_model == 3) {
             hipLaunchKernelGGL(k_alpha_warm_pts<3>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
-        else if (a.abs_model == 2)
+            hipLaunchKernelGGL(k_alpha_warm_big<3>, dim3(TORJ_WARM_BIG_GRID), dim3(64), 0, s2, a, sp);
+        } else if (a.abs_model == 2) {
             hipLaunchKernelGGL(k_alpha_warm_pts<1>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
+            hipLaunchKernelGGL(k_alpha_warm_big<1>, dim3(TORJ_WARM_BIG_GRID), dim3(64), 0, s2, a, sp);
+        }
         else if (sp.awork)  // a counted launch
             hipLaunchKernelGGL(k_alpha_pts<true>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         else

@@ -16,6 +16,44 @@
 
 namespace torj {
 
+// Region timers of the warm alpha kernel -- a profiling build only
+// (-DTORJ_WARM_PROF; scripts/mkvariant.py, tools/warm_prof.py), compiled out
+// otherwise.  TORJ_WPROF(k) charges the wave's wall clock since its previous
+// mark to region k; the first active lane keeps the stamps in LDS (one wave
+// per workgroup), k_alpha_warm_pts flushes them once per wave.
+#ifdef TORJ_WARM_PROF
+constexpr int kWProfN = 8;
+__device__ unsigned long long g_wprof[kWProfN + 1];
+#endif
+#if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+__shared__ unsigned long long s_wprof[kWProfN + 1];
+__device__ __forceinline__ bool wprof_leader() {
+    return (int)__lane_id() == __builtin_ffsll((long long)__ballot(1)) - 1;
+}
+__device__ __forceinline__ void wprof_mark(int k) {
+    const unsigned long long t = clock64();
+    if (wprof_leader()) {
+        s_wprof[1 + k] += t - s_wprof[0];
+        s_wprof[0] = t;
+    }
+}
+__device__ __forceinline__ void wprof_init() {
+    if (wprof_leader()) {
+        for (int k = 1; k <= kWProfN; k++) s_wprof[k] = 0;
+        s_wprof[0] = clock64();
+    }
+}
+__device__ __forceinline__ void wprof_flush() {
+    if (wprof_leader()) {
+        for (int k = 1; k <= kWProfN; k++) atomicAdd(&g_wprof[k], s_wprof[k]);
+        atomicAdd(&g_wprof[0], 1ull);
+    }
+}
+#define TORJ_WPROF(k) wprof_mark(k)
+#else
+#define TORJ_WPROF(k) ((void)0)
+#endif
+
 struct cplx {
     double re, im;
 };
@@ -44,12 +82,16 @@ TORJ_HD cplx operator+(cplx a, double s) { return {a.re + s, a.im}; }
 TORJ_HD cplx operator-(cplx a, double s) { return {a.re - s, a.im}; }
 TORJ_HD cplx I_times(cplx a) { return {-a.im, a.re}; }
 TORJ_HD double cabs_(cplx a) { return hypot(a.re, a.im); }
-TORJ_HD cplx csqrt_(cplx z) {  // principal branch, as Julia's sqrt(::ComplexF64)
+TORJ_HD double cnorm_(cplx a) { return fma(a.re, a.re, a.im * a.im); }  // |a|^2
+// principal branch, as Julia's sqrt(::ComplexF64), for the moderate operands of
+// warmdisp (|z| within 1e+-150: |z| from the sum of squares without hypot's
+// scaling, one reciprocal instead of two divisions; ~1 ulp)
+TORJ_HD cplx csqrt_(cplx z) {
     if (z.re == 0.0 && z.im == 0.0) return {0.0, z.im};
-    const double r = cabs_(z);
-    double t = sqrt(0.5 * (r + fabs(z.re)));
-    if (z.re >= 0.0) return {t, 0.5 * z.im / t};
-    return {0.5 * fabs(z.im) / t, copysign(t, z.im)};
+    const double r = sqrt_nn(cnorm_(z));
+    const double t = sqrt_nn(0.5 * (r + fabs(z.re))), h = 0.5 * rcp_nz(t);
+    if (z.re >= 0.0) return {t, z.im * h};
+    return {fabs(z.im) * h, copysign(t, z.im)};
 }
 
 constexpr double kSqrtPi = 1.7724538509055160272981674833411;
@@ -508,10 +550,25 @@ TORJ_HD void tensor_store(Tensor<L> &T, int l, double xg, double fl, const cplx 
 // reference's order.  Only the last three steps of the l-recurrence are
 // stored, so p / m are indexed statically and stay in registers.  The two
 // sides' Faddeeva evaluations run as interleaved pairs (zetac_upper2).
-TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx m[3]) {
-    const double anpl2hm1 = anpl * anpl / 2.0 - 1.0, psi = sqrt(0.5 * amu) * anpl, apsi = fabs(psi);
-    const bool big_psi = apsi > 0.7;
-    const double ipsi2 = big_psi ? 1.0 / (psi * psi) : 0.0, i2psi = big_psi ? 0.5 / psi : 0.0;
+// fsup's per-call invariants (the same for every |s|)
+struct WrInv {
+    double anpl2hm1, psi, ipsi2, i2psi;
+    bool big_psi;
+};
+TORJ_HD WrInv wr_inv(double anpl, double amu) {
+    WrInv v;
+    v.anpl2hm1 = anpl * anpl / 2.0 - 1.0;
+    v.psi = sqrt(0.5 * amu) * anpl;
+    v.big_psi = fabs(v.psi) > 0.7;
+    v.ipsi2 = v.big_psi ? 1.0 / (v.psi * v.psi) : 0.0;
+    v.i2psi = v.big_psi ? 0.5 / v.psi : 0.0;
+    return v;
+}
+TORJ_HD int fsup_s(double yg, double amu, const WrInv &iv, int isa, cplx p[3], cplx m[3]) {
+    TORJ_WPROF(3);  // (the previous |s|'s accumulation into ca)
+    const double anpl2hm1 = iv.anpl2hm1, psi = iv.psi;
+    const bool big_psi = iv.big_psi;
+    const double ipsi2 = iv.ipsi2, i2psi = iv.i2psi;
     for (int ir = 0; ir < 3; ir++) p[ir] = m[ir] = C(0.0);
     // side q = 0: is = -isa, q = 1: is = +isa (isa = 0: side 1 only; side 0
     // then repeats it as the partner of the pairs, and is not used)
@@ -544,6 +601,7 @@ TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx 
         for (int q = 0; q < 2; q++)
             cz[q][1] = mirror[q] ? C(-cz[q][0].re, cz[q][0].im) : zetac_upper(zx[q][1], zy[q][1]);
     }
+    TORJ_WPROF(1);  // the Faddeeva evaluations
     // Faddeeva evaluations of the reference's algorithm and those of them the
     // asymptotic series serves (the work counters, torj_hip/flops.py), packed
     // as nfad | nasym << 16
@@ -588,15 +646,62 @@ TORJ_HD int fsup_s(double yg, double anpl, double amu, int isa, cplx p[3], cplx 
             m[ir] = is > 0 ? m[ir] + cf2 : m[ir] - cf2;
         }
     }
+    TORJ_WPROF(2);  // the l-recurrences
     return nfad;
 }
 
 // weakly relativistic tensor (fsup + dieltens_maxw_wr, :473-638).  The |s|
 // loop runs outermost and adds its terms to every l >= |s|, in the
 // reference's summation order; ca[l][.] is indexed statically (registers).
+// The (|s|, l) coefficients of dieltens_maxw_wr's tensor sums (:598-627), a
+// compile-time table [|s|][l - 1][.]: is^2 a_sl, is l a_sl, b_sl, is a_sl,
+// l a_sl, a_sl with a_sl = (-1)^(l-|s|) / ((l+|s|)! (l-|s|)!) and
+// b_sl = a_sl (is^2 + 2 (l-|s|)(l-1)(l+|s|) / (2l-1)) -- each the value the
+// per-term expressions give (the same operations, rounded once at compile time)
+constexpr double cfact(int k) {
+    double f = 1.0;
+    for (int i = 2; i <= k; i++) f *= (double)i;
+    return f;
+}
+struct WrCoef {
+    double c[kWarmMaxL + 1][kWarmMaxL][6];
+    double fl[kWarmMaxL + 1];  // 0.5^l (2l)! / l! = (2l - 1)!!, exact
+};
+constexpr WrCoef make_wr_coef() {
+    WrCoef w{};
+    for (int isa = 0; isa <= kWarmMaxL; isa++)
+        for (int l = 1; l <= kWarmMaxL; l++) {
+            if (l < isa) continue;
+            const int lm = l - 1, k = l - isa;
+            const double is = isa;
+            const double asl = ((k & 1) ? -1.0 : 1.0) / (cfact(isa + l) * cfact(l - isa));
+            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + isa)) / (2 * l - 1));
+            double *c = w.c[isa][lm];
+            c[0] = (is * is) * asl;
+            c[1] = (is * l) * asl;
+            c[2] = bsl;
+            c[3] = is * asl;
+            c[4] = (double)l * asl;
+            c[5] = asl;
+        }
+    for (int l = 1; l <= kWarmMaxL; l++) {
+        double f = 1.0;
+        for (int j = 1; j <= l; j++) f *= (double)(2 * j - 1);
+        w.fl[l] = f;
+    }
+    return w;
+}
+#ifdef __HIP_DEVICE_COMPILE__
+__constant__ constexpr WrCoef kWrCoef = make_wr_coef();
+#else
+constexpr WrCoef kWrCoef = make_wr_coef();
+#endif
+
 template <int L>
 TORJ_HD int dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, Tensor<L> &T) {
     const double anpl2 = anpl * anpl;
+    const double iyg = 1.0 / yg, iyg2 = 1.0 / (yg * yg);  // operator/ (cplx, double)'s reciprocals
+    const WrInv iv = wr_inv(anpl, amu);
     cplx ca[L][6];
 #pragma unroll
     for (int l = 0; l < L; l++)
@@ -605,9 +710,8 @@ TORJ_HD int dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, 
     int nfad = 0;
     for (int isa = 0; isa <= lrm; isa++) {
         cplx p[3], m[3];
-        nfad += fsup_s(yg, anpl, amu, isa, p, m);
+        nfad += fsup_s(yg, amu, iv, isa, p, m);
         if (isa == 0) p0[0] = p[0], p0[1] = p[1], p0[2] = p[2];
-        const double is = isa;
         const cplx cq0p = amu * p[0], cq0m = amu * m[0];
         const cplx cq1p = amu * anpl * (p[0] - p[1]);
         const cplx cq1m = amu * anpl * (m[0] - m[1]);
@@ -615,26 +719,29 @@ TORJ_HD int dieltens_wr(double xg, double yg, double anpl, double amu, int lrm, 
 #pragma unroll
         for (int l = 1; l <= L; l++) {
             if (l > lrm || l < isa) continue;
-            const int lm = l - 1, k = l - isa;
-            const double asl = ((k & 1) ? -1.0 : 1.0) / (factd(isa + l) * factd(l - isa));
-            const double bsl = asl * (is * is + (double)(2 * k * lm * (l + isa)) / (2 * l - 1));
-            ca[lm][0] = ca[lm][0] + (is * is) * asl * cq0p;
-            ca[lm][1] = ca[lm][1] + (is * l) * asl * cq0m;
-            ca[lm][2] = ca[lm][2] + bsl * cq0p;
-            ca[lm][3] = ca[lm][3] + is * asl * cq1m / yg;
-            ca[lm][4] = ca[lm][4] + (double)l * asl * cq1p / yg;
-            ca[lm][5] = ca[lm][5] + asl * cq2p / (yg * yg);
+            const int lm = l - 1;
+            const double *c = kWrCoef.c[isa][lm];
+            ca[lm][0] = ca[lm][0] + c[0] * cq0p;
+            ca[lm][1] = ca[lm][1] + c[1] * cq0m;
+            ca[lm][2] = ca[lm][2] + c[2] * cq0p;
+            ca[lm][3] = ca[lm][3] + (c[3] * cq1m) * iyg;
+            ca[lm][4] = ca[lm][4] + (c[4] * cq1p) * iyg;
+            ca[lm][5] = ca[lm][5] + (c[5] * cq2p) * iyg2;
         }
     }
+    TORJ_WPROF(3);
+    // f_l = 0.5^l (1 / yg^2 / amu)^(l-1) (2l)! / l!: the power by products
+    const double u = iyg * iyg / amu;
+    double upow = 1.0;
 #pragma unroll
     for (int l = 1; l <= L; l++) {
         if (l > lrm) break;
-        const int lm = l - 1;
-        const double fcl = pow(0.5, l) * pow((1.0 / yg) * (1.0 / yg) / amu, lm) * factd(2 * l) / factd(l);
-        tensor_store(T, l, xg, fcl, ca[lm]);
+        if (l > 1) upow *= u;
+        tensor_store(T, l, xg, kWrCoef.fl[l] * upow, ca[l - 1]);
     }
     const cplx cq2p = p0[1] + amu * anpl2 * (p0[2] + p0[0] - 2.0 * p0[1]);
     T.e330 = 1.0 - xg * amu * cq2p;
+    TORJ_WPROF(4);  // the l-factors and the tensor's store
     return nfad;
 }
 
@@ -798,10 +905,13 @@ TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int so
                           const Tensor<L> &T, int &passes) {
     cplx anpr2a = C(anprc * anprc), anpr2 = anpr2a;
     const double anpl2 = anpl * anpl;
-    double errnpr = 1.0;
-    passes = 0;  // tensor sums evaluated (the work counters)
+    double errnpr = 1.0, na = cnorm_(anpr2a);  // |anpr2a|^2
+    passes = 0;  // passes of the reference's loop, the breaking one included (the work counters)
     for (int i = 1; i <= 100; i++) {
         passes = i;
+        // the reference sums the tensor before this test, for the polarisation
+        // of its breaking pass (:1172-1196); alpha needs N_perp^2 only
+        if (i > 2 && errnpr < 1.0e-4) break;
         cplx s[6] = {C(0), C(0), C(0), C(0), C(0), C(0)};
         cplx pw = C(1.0);
 #pragma unroll
@@ -813,7 +923,6 @@ TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int so
         // diagonal identity terms for l = 1 are already in T.e[0]
         const cplx e11 = s[0], e12 = s[1], e22 = s[2], a13 = s[3], a23 = s[4], a33 = s[5];
         const cplx a31 = a13, a32 = -a23;
-        if (i > 2 && errnpr < 1.0e-4) break;
         const cplx cc4 = (e11 - anpl2) * (1.0 - a33) + (a13 + anpl) * (a31 + anpl);
         const cplx cc2 = -e12 * e12 * (1.0 - a33) - a32 * e12 * (a13 + anpl) + a23 * e12 * (a31 + anpl) -
                          (a23 * a32 + T.e330 + (e22 - anpl2) * (1.0 - a33)) * (e11 - anpl2) -
@@ -828,11 +937,17 @@ TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int so
             sg = (double)(-sox);
             if (rr.re <= 0.0 && rr.im >= 0.0) sg = -sg;
         }
-        anpr2 = (-cc2 + sg * csqrt_(rr)) / (2.0 * cc4);
-        errnpr = fabs(1.0 - cabs_(anpr2) / cabs_(anpr2a));
+        // (-cc2 + sg sqrt(rr)) / (2 cc4) as a product with conj(cc4) / (2 |cc4|^2)
+        const double ic = 0.5 * rcp_nz(cnorm_(cc4));
+        anpr2 = (-cc2 + sg * csqrt_(rr)) * C(cc4.re * ic, -cc4.im * ic);
+        // |1 - |anpr2| / |anpr2a||, the moduli from their squares
+        const double n2 = cnorm_(anpr2);
+        errnpr = fabs(1.0 - sqrt_nn(n2 * rcp_nz(na)));
         anpr2a = anpr2;
+        na = n2;
     }
     if (anpr2.re < 0.0 && anpr2.im < 0.0) anpr2 = C(0.0);  // ierr = 99
+    TORJ_WPROF(5);  // warmdisp
     return anpr2;
 }
 
@@ -909,23 +1024,42 @@ TORJ_HD WarmAlpha alpha_core(double omega, double X, double Y, double N_par, dou
 // The tensor is sized for lrm <= 3 (the common case: one to three Larmor
 // orders up to the third harmonic) or lrm <= 5; on the device the choice is
 // made per wave (ballot), so the heavy code never diverges between the two.
+// (The split pipeline's k_alpha_warm_pts instead defers its lrm > 3 points to
+// k_alpha_warm_big, so that its own registers are sized for lrm <= 3.)
+// The call's setup (alpha, :1328-1337, up to the tensor): mu, N_perp of the
+// cold root and the Larmor order by larmornumber
+struct WarmSetup {
+    double mu, npr;
+    int lrm, ltrips;
+};
+TORJ_HD WarmSetup warm_setup(double Y, double N_abs, double N_par, double Te) {
+    WarmSetup w;
+    w.mu = kMe * kC * kC / (Te * kE);
+    w.npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
+    const int nharm = larmornumber(Y, N_par, w.mu, w.ltrips);
+    w.lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
+    TORJ_WPROF(0);  // inputs, larmornumber
+    return w;
+}
+// the rest of the call with the tensor sized for lrm <= L
+template <int IWARM, int L>
+TORJ_HD WarmAlpha alpha_warm_l(double omega, double X, double Y, double N_par, const WarmSetup &w,
+                               double inv_dDdN, int mode) {
+    WarmAlpha r = alpha_core<IWARM, L>(omega, X, Y, N_par, w.mu, w.npr, w.lrm, inv_dDdN, mode);
+    r.ltrips = w.ltrips;
+    return r;
+}
 template <int IWARM>
 TORJ_WARM_ATTR WarmAlpha alpha_warm_v(double omega, double X, double Y, double N_abs, double N_par,
                                       double Te, double inv_dDdN, int mode) {
-    const double mu = kMe * kC * kC / (Te * kE);
-    const double npr = sqrt(fmax(N_abs * N_abs - N_par * N_par, 0.0));
-    int ltrips;
-    const int nharm = larmornumber(Y, N_par, mu, ltrips);
-    const int lrm = nharm < kWarmMaxL ? nharm : kWarmMaxL;
+    const WarmSetup w = warm_setup(Y, N_abs, N_par, Te);
 #if defined(__HIP_DEVICE_COMPILE__)
-    const bool big = __ballot(lrm > 3) != 0;
+    const bool big = __ballot(w.lrm > 3) != 0;
 #else
-    const bool big = lrm > 3;
+    const bool big = w.lrm > 3;
 #endif
-    WarmAlpha r = big ? alpha_core<IWARM, kWarmMaxL>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode)
-                      : alpha_core<IWARM, 3>(omega, X, Y, N_par, mu, npr, lrm, inv_dDdN, mode);
-    r.ltrips = ltrips;
-    return r;
+    return big ? alpha_warm_l<IWARM, kWarmMaxL>(omega, X, Y, N_par, w, inv_dDdN, mode)
+               : alpha_warm_l<IWARM, 3>(omega, X, Y, N_par, w, inv_dDdN, mode);
 }
 
 template <int IWARM>

@@ -76,7 +76,7 @@ def algorithmic_flops_reference(counters, n_gl: int = 24) -> float:
 # (same convention; factorial tables and loop invariants not counted; branch-
 # dependent parts at their cheapest branch, so the model is a lower bound: 97.5-
 # 99.8 % of the instrumented count, tests/test_warm_flops.py).
-FLOPS_WARM_CALL = 77          # Te, |N|, mu, N_perp, per-call invariants, e330, alpha
+FLOPS_WARM_CALL = 80          # Te, |N|, mu, N_perp, per-call invariants, e330, alpha
 FLOPS_WARM_LARMOR_TEST = 10   # per larmornumber resonance test
 FLOPS_WARM_FADDEEVA = 278     # per Z(z) by Weideman's N = 36 complex Horner sum (|z| < 16)
 FLOPS_WARM_FADDEEVA_ASYM = 102  # per Z(z) by the asymptotic series (|x| or Im z >= 16), 10 terms
@@ -86,8 +86,8 @@ FLOPS_WARM_STORE = 4          # per stored recursion step: cefp, cefm accumulati
 FLOPS_WARM_ISA = 22           # per |s|: cq0p .. cq2p
 FLOPS_WARM_PAIR = 27          # per (|s|, l) term of the tensor sums
 FLOPS_WARM_ORDER = 15         # per Larmor order l: f_l and the six components
-FLOPS_WARM_SUM_TERM = 54      # per warmdisp pass and order: sum eps_l N_perp^(2l)
-FLOPS_WARM_UPDATE = 168       # per warmdisp update: cc4, cc2, cc0, root, convergence
+FLOPS_WARM_SUM_TERM = 54      # per warmdisp update and order: sum eps_l N_perp^(2l)
+FLOPS_WARM_UPDATE = 167       # per warmdisp update: cc4, cc2, cc0, root, convergence
 
 
 def algorithmic_flops_warm(counters) -> float:
@@ -103,9 +103,10 @@ def algorithmic_flops_warm(counters) -> float:
     stored = 6.0 * sl + 2.0 * calls
     pairs = 0.5 * (sl2 + 3.0 * sl)            # (|s|, l), max(|s|, 1) <= l <= lrm
     updates = passes - calls                  # every pass but the breaking one
+    sums = pass_l - sl                        # the breaking pass sums no tensor (torj_warm.hpp warmdisp_n2)
     return (steps * FLOPS_STEP_OVERHEAD + calls * (FLOPS_RHS_COLD + FLOPS_WARM_CALL)
             + tests * FLOPS_WARM_LARMOR_TEST + (fad - asym) * FLOPS_WARM_FADDEEVA
             + asym * FLOPS_WARM_FADDEEVA_ASYM
             + sides * FLOPS_WARM_SIDE + rsteps * FLOPS_WARM_STEP + stored * FLOPS_WARM_STORE
             + (sl + calls) * FLOPS_WARM_ISA + pairs * FLOPS_WARM_PAIR + sl * FLOPS_WARM_ORDER
-            + pass_l * FLOPS_WARM_SUM_TERM + updates * FLOPS_WARM_UPDATE)
+            + sums * FLOPS_WARM_SUM_TERM + updates * FLOPS_WARM_UPDATE)
