@@ -47,7 +47,7 @@ FLOP_MODEL = {"albajar": "albajar-v3 (round 3: exact-zero, negligible and settle
                          "harmonics priced at their tests)",
               "none": "albajar-v3",
               "warm_wr": "warm-v3 (round 5: warmdisp's breaking pass sums no tensor, its root by "
-                         "the conjugate product; round 3: counter[2] = asymptotic Faddeeva "
+                         "the conjugate product, the asymptotic Faddeeva series by Horner; round 3: counter[2] = asymptotic Faddeeva "
                          "evaluations; larmornumber tests priced at one per call, a lower bound)"}
 ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)",
               "warm_wr": "warm weakly-relativistic alpha (iwarm=1)",

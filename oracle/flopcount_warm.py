@@ -166,10 +166,10 @@ def faddeeva_asym_count():
     ir2 = 1.0 / (x * x + y * y)
     a, b = x * ir2, -y * ir2
     ur, ui = 0.5 * (a * a - b * b), a * b
-    tr, ti = CF(1.0), CF(0.0)
-    for j in range(KFAD_ASYM_K - 1, 0, -1):
-        vr, vi = ur * tr - ui * ti, ur * ti + ui * tr
-        tr, ti = (2 * j - 1) * vr + 1.0, (2 * j - 1) * vi
+    # Horner in u with the (2k - 1)!! as constants (torj_warm.hpp faddeeva_asym)
+    tr, ti = CF(34459425.0), CF(0.0)
+    for k in range(KFAD_ASYM_K - 2, -1, -1):
+        tr, ti = tr * ur + (-ti * ui + float(math.prod(range(1, 2 * k, 2)))), tr * ui + ti * ur
     pr, pim = a * tr - b * ti, a * ti + b * tr
     _ = (-0.56 * pim, 0.56 * pr)
     _ = (-1.77 * _[1], 1.77 * _[0])

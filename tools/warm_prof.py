@@ -40,13 +40,22 @@ def main():
     buf = (ctypes.c_ulonglong * 9)()
     T.trace(P, xp, Np, om, 1, ds=1e-4, n_steps=n_steps, absorption=2)  # warm-up
     rd(buf)
+    L.torj_warm_fad_read((ctypes.c_ulonglong * 9)())
     T.trace(P, xp, Np, om, 1, ds=1e-4, n_steps=n_steps, absorption=2)
     rd(buf)
     v = np.array(buf[:], dtype=np.float64)
+    fr = L.torj_warm_fad_read
+    fr.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+    fb = (ctypes.c_ulonglong * 9)()
+    fr(fb)
+    f = [int(x) for x in fb]
     tot = v[1:].sum()
     out = {"waves": int(v[0]), "rays": len(w), "n_steps": n_steps,
            "regions": {REGIONS[k]: {"ticks_per_wave": v[1 + k] / max(v[0], 1), "share": v[1 + k] / tot}
                        for k in range(8) if v[1 + k] > 0}}
+    out["faddeeva_pairs"] = {"wave_calls": f[0], "wave_calls_with_weideman": f[1],
+                             "lane_calls": f[2], "lane_calls_with_weideman": f[3],
+                             "weideman_args_by_z2": dict(zip(["<36", "<64", "<100", "<144", "<256"], f[4:9]))}
     print(json.dumps(out, indent=1))
 
 

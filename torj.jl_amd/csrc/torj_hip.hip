@@ -1290,6 +1290,15 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
     // alpha the scan never reads
     if (sp.k0 + j >= info_steps(ti) || info_status(si) != ST_OK) return;
+#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    {
+        const unsigned long long am = __ballot(1);
+        if ((int)__lane_id() == __builtin_ffsll((long long)am) - 1) {
+            atomicAdd(&g_aprof[4], 1ull);
+            atomicAdd(&g_aprof[5], (unsigned long long)__popcll(am));
+        }
+    }
+#endif
     const double Nabs = sqrt_pos(N2), Te = exp_fast(lnTe);
     if constexpr (COUNT) {
         AlbajarWork work = {};
@@ -1321,13 +1330,16 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 // at 128 and 149.0 at 256, alternating)
 #endif
 constexpr int kAlphaWarmBlock = TORJ_ALPHA_WARM_BLOCK;
+// COUNT: a counted launch (sp.awork set) stores the work word; without it the
+// trip counts are dead and the compiler drops their arithmetic
+template <bool COUNT>
 __device__ __forceinline__ void warm_store(const SplitArgs &sp, int js, int i, int n, const WarmAlpha &r) {
     sp.alpha[(size_t)js * n + i] = r.alpha;
-    if (sp.awork)
+    if constexpr (COUNT)
         sp.awork[(size_t)js * n + i] = (unsigned)min(r.nasym, 127) | ((unsigned)min(r.nfad, 127) << 7) |
                                    ((unsigned)min(r.passes, 127) << 14) | ((unsigned)r.lrm << 21);
 }
-template <int IWARM>
+template <int IWARM, bool COUNT>
 __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
     k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
     const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
@@ -1362,7 +1374,7 @@ __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA
     }
     if (big) return;
     const WarmAlpha r = alpha_warm_l<IWARM, 3>(a.omega, X, Y, Npar, w, inv, a.mode);
-    warm_store(sp, js, i, a.n, r);
+    warm_store<COUNT>(sp, js, i, a.n, r);
 #if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
     TORJ_WPROF(6);  // the stores
     wprof_flush();
@@ -1374,7 +1386,7 @@ __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA
 #ifndef TORJ_WARM_BIG_GRID
 #define TORJ_WARM_BIG_GRID 512  // workgroups of 64: two waves per CU
 #endif
-template <int IWARM>
+template <int IWARM, bool COUNT>
 __global__ void __launch_bounds__(64) k_alpha_warm_big(TraceArgs a, SplitArgs sp) {
     const unsigned cnt = *sp.defer_cnt;
     for (unsigned k = blockIdx.x * 64 + threadIdx.x; k < cnt; k += gridDim.x * 64) {
@@ -1385,7 +1397,7 @@ __global__ void __launch_bounds__(64) k_alpha_warm_big(TraceArgs a, SplitArgs sp
         const WarmSetup w = warm_setup(in[(size_t)a.n], in[2 * (size_t)a.n], Npar, in[4 * (size_t)a.n]);
         const WarmAlpha r = alpha_warm_l<IWARM, kWarmMaxL>(a.omega, in[0], in[(size_t)a.n], Npar, w,
                                                             in[5 * (size_t)a.n], a.mode);
-        warm_store(sp, js, i, a.n, r);
+        warm_store<COUNT>(sp, js, i, a.n, r);
     }
 }
 
@@ -2359,6 +2371,16 @@ int torj_abi_version(void) { return TORJ_ABI_VERSION; }
 #endif
 const char *torj_build_id(void) { return TORJ_BUILD_ID; }
 
+#ifdef TORJ_ALPHA_PROF
+// profiling build only (not in include/torj_hip.h): g_aprof, read and reset
+int torj_alpha_prof_read(unsigned long long *out) {
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_aprof), sizeof(g_aprof)));
+    static const unsigned long long zero[8] = {};
+    HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_aprof), zero, sizeof(g_aprof)));
+    return 0;
+}
+#endif
 #ifdef TORJ_WARM_PROF
 // profiling build only (not in include/torj_hip.h): the warm alpha's region
 // timers -- out[0] waves, out[1 + k] clock ticks of region k -- read and reset
@@ -2367,6 +2389,13 @@ int torj_warm_prof_read(unsigned long long *out) {
     HIPCK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wprof), sizeof(g_wprof)));
     static const unsigned long long zero[kWProfN + 1] = {};
     HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_wprof), zero, sizeof(g_wprof)));
+    return 0;
+}
+int torj_warm_fad_read(unsigned long long *out) {
+    HIPCK(hipDeviceSynchronize());
+    HIPCK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_wfad), sizeof(g_wfad)));
+    static const unsigned long long zero[9] = {};
+    HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_wfad), zero, sizeof(g_wfad)));
     return 0;
 }
 #endif
@@ -3034,13 +3063,19 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const int nqW = (int)((n + kAlphaWarmBlock - 1) / kAlphaWarmBlock);
         const dim3 agridW((unsigned)(nqW * 4 * sp.kb));
         sp.defer_cnt = dcnt ? dcnt + b : nullptr;
+#define TORJ_WARM_LAUNCH(IW, C)                                                                     \
+    do {                                                                                            \
+        hipLaunchKernelGGL((k_alpha_warm_pts<IW, C>), agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW); \
+        hipLaunchKernelGGL((k_alpha_warm_big<IW, C>), dim3(TORJ_WARM_BIG_GRID), dim3(64), 0, s2, a, sp); \
+    } while (0)
         if (a.abs_model == 3) {
-            hipLaunchKernelGGL(k_alpha_warm_pts<3>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
-            hipLaunchKernelGGL(k_alpha_warm_big<3>, dim3(TORJ_WARM_BIG_GRID), dim3(64), 0, s2, a, sp);
+            if (sp.awork) TORJ_WARM_LAUNCH(3, true);
+            else TORJ_WARM_LAUNCH(3, false);
         } else if (a.abs_model == 2) {
-            hipLaunchKernelGGL(k_alpha_warm_pts<1>, agridW, dim3(kAlphaWarmBlock), 0, s2, a, sp, nqW);
-            hipLaunchKernelGGL(k_alpha_warm_big<1>, dim3(TORJ_WARM_BIG_GRID), dim3(64), 0, s2, a, sp);
+            if (sp.awork) TORJ_WARM_LAUNCH(1, true);
+            else TORJ_WARM_LAUNCH(1, false);
         }
+#undef TORJ_WARM_LAUNCH
         else if (sp.awork)  // a counted launch
             hipLaunchKernelGGL(k_alpha_pts<true>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         else

@@ -1128,6 +1128,12 @@ TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, doub
     return g;
 }
 
+#ifdef TORJ_ALPHA_PROF
+// profiling build only (tools/alpha_prof.py): [2 (m - 2)] waves and [2 (m - 2) + 1]
+// lanes that ran harmonic m's node loop, [4] waves and [5] live lanes of k_alpha_pts
+__device__ unsigned long long g_aprof[8];
+#endif
+
 // Work counters of one lane (include/torj_hip.h torj_trace: counters[2..7]).
 // Albajar (ABS 1) / warm weakly relativistic (ABS 2, torj_warm.hpp) meaning:
 struct AlbajarWork {
@@ -1219,6 +1225,15 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
             return 0.0;
         }
     }
+#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    {  // profiling build only: node loops run per wave and per lane (lane utilisation)
+        const unsigned long long am = __ballot(1);
+        if ((int)__lane_id() == __builtin_ffsll((long long)am) - 1) {
+            atomicAdd(&g_aprof[2 * (M - 2)], 1ull);
+            atomicAdd(&g_aprof[2 * (M - 2) + 1], (unsigned long long)__popcll(am));
+        }
+    }
+#endif
     if (work) {
         constexpr int kTerms[5] = {series_terms(0), series_terms(1), series_terms(2), series_terms(3),
                                    kSeriesSlow};

@@ -24,6 +24,7 @@ namespace torj {
 #ifdef TORJ_WARM_PROF
 constexpr int kWProfN = 8;
 __device__ unsigned long long g_wprof[kWProfN + 1];
+__device__ unsigned long long g_wfad[9];  // faddeeva_upper2's branch statistics (see there)
 #endif
 #if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
 __shared__ unsigned long long s_wprof[kWProfN + 1];
@@ -412,18 +413,25 @@ TORJ_HD cplx faddeeva(double xi, double yi) {
 // about half the Weideman cost: C5 trace phase 162.1 -> 143.8 ms.
 constexpr double kFadAsym = 16.0;
 constexpr int kFadAsymK = 10;
+constexpr double dfact_odd(int k) {  // (2k - 1)!!, (-1)!! = 1: exact below 2^53
+    double f = 1.0;
+    for (int j = 1; j <= k; j++) f *= (double)(2 * j - 1);
+    return f;
+}
 TORJ_HD bool faddeeva_asym_ok(double x, double y) { return fabs(x) >= kFadAsym || y >= kFadAsym; }
 TORJ_HD cplx faddeeva_asym(double x, double y) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
     const double ir2 = rcp_nz(fma(x, x, y * y));
     const double a = x * ir2, b = -y * ir2;  // 1 / z
     const double ur = 0.5 * fma(a, a, -b * b), ui = a * b;  // u = (1 / z)^2 / 2
-    double tr = 1.0, ti = 0.0;
+    // T = sum_{k < K} (2k - 1)!! u^k by Horner with the double factorials as
+    // constants (4 VALU per term; the nested 1 + (2j - 1) u (...) form took 6)
+    double tr = dfact_odd(kFadAsymK - 1), ti = 0.0;
 #pragma unroll
-    for (int j = kFadAsymK - 1; j >= 1; j--) {  // T = 1 + (2j - 1) u T
-        const double vr = fma(ur, tr, -ui * ti), vi = fma(ur, ti, ui * tr);
-        tr = fma((double)(2 * j - 1), vr, 1.0);
-        ti = (double)(2 * j - 1) * vi;
+    for (int k = kFadAsymK - 2; k >= 0; k--) {  // T = T u + (2k - 1)!!
+        const double t = fma(tr, ur, fma(-ti, ui, dfact_odd(k)));
+        ti = fma(tr, ui, ti * ur);
+        tr = t;
     }
     const double pr = fma(a, tr, -b * ti), pim = fma(a, ti, b * tr);  // T / z
     cplx w;
@@ -470,6 +478,25 @@ TORJ_HD cplx faddeeva_upper(double x, double y) {
 TORJ_HD void faddeeva_upper2(double x0, double y0, double x1, double y1, cplx &w0, cplx &w1) {
     constexpr double kInvSqrtPi = 0.56418958354775628695;
     const bool a0 = faddeeva_asym_ok(x0, y0), a1 = faddeeva_asym_ok(x1, y1);
+#if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
+    {  // profiling build: pair calls per wave -- all lanes asymptotic / some lane Weideman,
+       // and lanes with a Weideman argument; plus |z|^2 of those in bins [<36, <64, <100, <144, <256]
+        const unsigned long long am = __ballot(1), wm = __ballot(!(a0 && a1));
+        if ((int)__lane_id() == __builtin_ffsll((long long)am) - 1) {
+            atomicAdd(&g_wfad[0], 1ull);
+            atomicAdd(&g_wfad[1], wm ? 1ull : 0ull);
+            atomicAdd(&g_wfad[2], (unsigned long long)__popcll(am));
+            atomicAdd(&g_wfad[3], (unsigned long long)__popcll(wm));
+        }
+        const double zz[2] = {x0 * x0 + y0 * y0, x1 * x1 + y1 * y1};
+        const bool aa[2] = {a0, a1};
+        for (int q = 0; q < 2; q++)
+            if (!aa[q]) {
+                const int b = zz[q] < 36 ? 0 : zz[q] < 64 ? 1 : zz[q] < 100 ? 2 : zz[q] < 144 ? 3 : 4;
+                atomicAdd(&g_wfad[4 + b], 1ull);
+            }
+    }
+#endif
     if (a0 || a1) {  // the same branches as faddeeva_upper, so the same bits
         w0 = a0 ? faddeeva_asym(x0, y0) : faddeeva_upper(x0, y0);
         w1 = a1 ? faddeeva_asym(x1, y1) : faddeeva_upper(x1, y1);
@@ -558,7 +585,7 @@ struct WrInv {
 TORJ_HD WrInv wr_inv(double anpl, double amu) {
     WrInv v;
     v.anpl2hm1 = anpl * anpl / 2.0 - 1.0;
-    v.psi = sqrt(0.5 * amu) * anpl;
+    v.psi = sqrt_nn(0.5 * amu) * anpl;
     v.big_psi = fabs(v.psi) > 0.7;
     v.ipsi2 = v.big_psi ? 1.0 / (v.psi * v.psi) : 0.0;
     v.i2psi = v.big_psi ? 0.5 / v.psi : 0.0;
@@ -578,7 +605,7 @@ TORJ_HD int fsup_s(double yg, double amu, const WrInv &iv, int isa, cplx p[3], c
         const int is = q == 0 ? -isa : isa;
         alpha[q] = anpl2hm1 + is * yg;
         phi2[q] = amu * alpha[q];
-        phim[q] = sqrt(fabs(phi2[q]));
+        phim[q] = sqrt_nn(fabs(phi2[q]));
         if (alpha[q] >= 0) {
             zx[q][0] = psi - phim[q], zy[q][0] = 0.0, zx[q][1] = -psi - phim[q], zy[q][1] = 0.0;
             zx[q][2] = -phim[q], zy[q][2] = 0.0;
@@ -592,14 +619,21 @@ TORJ_HD int fsup_s(double yg, double amu, const WrInv &iv, int isa, cplx p[3], c
     // so Z(z_m) = -conj(Z(z_p)) and one evaluation serves both.
     const bool mirror[2] = {alpha[0] < 0, alpha[1] < 0};
     cplx cz[2][3];
-    zetac_upper2(zx[0][0], zy[0][0], zx[1][0], zy[1][0], cz[0][0], cz[1][0]);
-    if (!big_psi) zetac_upper2(zx[0][2], zy[0][2], zx[1][2], zy[1][2], cz[0][2], cz[1][2]);
-    if (!mirror[0] && !mirror[1]) {
-        zetac_upper2(zx[0][1], zy[0][1], zx[1][1], zy[1][1], cz[0][1], cz[1][1]);
+    if (isa == 0) {  // one side (s = 0; isa is the caller's loop counter: wave-uniform)
+        cz[1][0] = zetac_upper(zx[1][0], zy[1][0]);
+        if (!big_psi) cz[1][2] = zetac_upper(zx[1][2], zy[1][2]);
+        cz[1][1] = mirror[1] ? C(-cz[1][0].re, cz[1][0].im) : zetac_upper(zx[1][1], zy[1][1]);
+        cz[0][0] = cz[1][0], cz[0][1] = cz[1][1], cz[0][2] = cz[1][2];  // (side 0 unused)
     } else {
+        zetac_upper2(zx[0][0], zy[0][0], zx[1][0], zy[1][0], cz[0][0], cz[1][0]);
+        if (!big_psi) zetac_upper2(zx[0][2], zy[0][2], zx[1][2], zy[1][2], cz[0][2], cz[1][2]);
+        if (!mirror[0] && !mirror[1]) {
+            zetac_upper2(zx[0][1], zy[0][1], zx[1][1], zy[1][1], cz[0][1], cz[1][1]);
+        } else {
 #pragma unroll
-        for (int q = 0; q < 2; q++)
-            cz[q][1] = mirror[q] ? C(-cz[q][0].re, cz[q][0].im) : zetac_upper(zx[q][1], zy[q][1]);
+            for (int q = 0; q < 2; q++)
+                cz[q][1] = mirror[q] ? C(-cz[q][0].re, cz[q][0].im) : zetac_upper(zx[q][1], zy[q][1]);
+        }
     }
     TORJ_WPROF(1);  // the Faddeeva evaluations
     // Faddeeva evaluations of the reference's algorithm and those of them the
