@@ -1206,15 +1206,30 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         if (cw * ch > sp.tile_cap) {
             tc.cw = tc.ch = 0;  // too wide for the tile: every cell from global memory
         } else {
-            // one cell record (48 x 16 B) per pass, lanes 0..47
-            const int cR = a.g.nR - 1;
+            // the tile's 16-byte pieces (48 per cell record) over the 64 lanes,
+            // four loads in flight per lane before their LDS stores (a loop of
+            // one record per pass waited out one memory latency per cell)
+            const int cR = a.g.nR - 1, np = cw * ch * (kCellRec / 2);
             const Dbl2 *src = reinterpret_cast<const Dbl2 *>(a.cellp);
             Dbl2 *dst = reinterpret_cast<Dbl2 *>(s_cell);
-            for (int zr = 0; zr < ch; zr++)
-                for (int rr = 0; rr < cw; rr++)
-                    if (threadIdx.x < kCellRec / 2)
-                        dst[(zr * cw + rr) * (kCellRec / 2) + threadIdx.x] =
-                            src[((size_t)(cZ0 + zr) * cR + cR0 + rr) * (kCellRec / 2) + threadIdx.x];
+            constexpr int kP = kCellRec / 2, kU = 4;
+            for (int k0 = 0; k0 < np; k0 += 64 * kU) {
+                Dbl2 v[kU];
+                int kk[kU];
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const int k = k0 + u * 64 + (int)threadIdx.x;
+                    kk[u] = k;
+                    if (k < np) {
+                        const int cell = k / kP, piece = k - cell * kP;
+                        const int zr = cell / cw, rr = cell - zr * cw;
+                        v[u] = src[((size_t)(cZ0 + zr) * cR + cR0 + rr) * kP + piece];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kU; u++)
+                    if (kk[u] < np) dst[kk[u]] = v[u];
+            }
         }
         __syncthreads();
         if (!live) return;
@@ -1286,6 +1301,9 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
     const double X = in[0], Y = in[(size_t)a.n], N2 = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
     const double lnTe = in[4 * (size_t)a.n];
+    // (an empty asm that consumes them: the compiler would otherwise sink the
+    // input loads below the stop test and the Te test, three latencies in a row)
+    asm volatile("" ::"v"(ti), "v"(si), "v"(X), "v"(Y), "v"(N2), "v"(Npar), "v"(lnTe));
     // sinfo may be stale (k_tau_scan of an earlier block runs on another
     // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
     // alpha the scan never reads
@@ -1351,6 +1369,7 @@ __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA
     const double *in = sp.ain + (size_t)js * kAinFW * a.n + i;
     const double X = in[0], Y = in[(size_t)a.n], Nabs = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
     const double Te = in[4 * (size_t)a.n], inv = in[5 * (size_t)a.n];
+    asm volatile("" ::"v"(ti), "v"(si), "v"(X), "v"(Y), "v"(Nabs), "v"(Npar), "v"(Te), "v"(inv));
     if (sp.k0 + j >= info_steps(ti) || info_status(si) != ST_OK) return;
 #if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
     static_assert(kAlphaWarmBlock == 64, "region timers: one wave per workgroup");
