@@ -1206,30 +1206,16 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         if (cw * ch > sp.tile_cap) {
             tc.cw = tc.ch = 0;  // too wide for the tile: every cell from global memory
         } else {
-            // the tile's 16-byte pieces (48 per cell record) over the 64 lanes,
-            // four loads in flight per lane before their LDS stores (a loop of
-            // one record per pass waited out one memory latency per cell)
-            const int cR = a.g.nR - 1, np = cw * ch * (kCellRec / 2);
+            // one cell record (48 x 16 B) per pass, lanes 0..47 (measured: four
+            // loads in flight per lane over the flattened tile is no faster)
+            const int cR = a.g.nR - 1;
             const Dbl2 *src = reinterpret_cast<const Dbl2 *>(a.cellp);
             Dbl2 *dst = reinterpret_cast<Dbl2 *>(s_cell);
-            constexpr int kP = kCellRec / 2, kU = 4;
-            for (int k0 = 0; k0 < np; k0 += 64 * kU) {
-                Dbl2 v[kU];
-                int kk[kU];
-#pragma unroll
-                for (int u = 0; u < kU; u++) {
-                    const int k = k0 + u * 64 + (int)threadIdx.x;
-                    kk[u] = k;
-                    if (k < np) {
-                        const int cell = k / kP, piece = k - cell * kP;
-                        const int zr = cell / cw, rr = cell - zr * cw;
-                        v[u] = src[((size_t)(cZ0 + zr) * cR + cR0 + rr) * kP + piece];
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < kU; u++)
-                    if (kk[u] < np) dst[kk[u]] = v[u];
-            }
+            for (int zr = 0; zr < ch; zr++)
+                for (int rr = 0; rr < cw; rr++)
+                    if (threadIdx.x < kCellRec / 2)
+                        dst[(zr * cw + rr) * (kCellRec / 2) + threadIdx.x] =
+                            src[((size_t)(cZ0 + zr) * cR + cR0 + rr) * (kCellRec / 2) + threadIdx.x];
         }
         __syncthreads();
         if (!live) return;
