@@ -933,6 +933,23 @@ TORJ_HD void dieltens_fr(double xg, double yg, double anpl, double amu, int lrm,
     T.e330 = C(1.0 + xg * rr[3][2][0]);
 }
 
+#ifndef TORJ_WARM_RR_COMP
+#define TORJ_WARM_RR_COMP 0
+#endif
+// a0 b0 + a1 b1 + a2 b2 + a3 b3 as if in twice the working precision (Ogita,
+// Rump & Oishi's Dot2: error-free products by fma, error-free sums)
+TORJ_HD double dot2_4(const double (&a)[4], const double (&b)[4]) {
+    double p = a[0] * b[0], s = fma(a[0], b[0], -p);
+#pragma unroll
+    for (int k = 1; k < 4; k++) {
+        const double h = a[k] * b[k], r = fma(a[k], b[k], -h);
+        const double t = p + h, z = t - p, q = (p - (t - z)) + (h - z);
+        p = t;
+        s += q + r;
+    }
+    return p + s;
+}
+
 // warmdisp (:1158-1267) -> N_perp^2 (complex); anpr2 initialised (R2)
 template <int L>
 TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int sox, int lrm,
@@ -962,7 +979,16 @@ TORJ_HD cplx warmdisp_n2(double xg, double yg, double anpl, double anprc, int so
                          (a23 * a32 + T.e330 + (e22 - anpl2) * (1.0 - a33)) * (e11 - anpl2) -
                          (a13 + anpl) * (a31 + anpl) * (e22 - anpl2);
         const cplx cc0 = T.e330 * ((e11 - anpl2) * (e22 - anpl2) + e12 * e12);
+#if TORJ_WARM_RR_COMP
+        // R6 (an A/B, off by default): the discriminant in twice the working
+        // precision (Dot2), so that its own cancellation cannot decide the root
+        // selector below
+        const double ar[4] = {cc2.re, cc2.im, cc0.re, cc0.im}, br[4] = {cc2.re, -cc2.im, -4.0 * cc4.re, 4.0 * cc4.im};
+        const double ai[4] = {2.0 * cc2.re, cc0.re, cc0.im, 0.0}, bi[4] = {cc2.im, -4.0 * cc4.im, -4.0 * cc4.re, 0.0};
+        const cplx rr = C(dot2_4(ar, br), dot2_4(ai, bi));
+#else
         const cplx rr = cc2 * cc2 - 4.0 * cc0 * cc4;
+#endif
         double sg;
         if (yg > 1.0) {
             sg = (double)sox;
