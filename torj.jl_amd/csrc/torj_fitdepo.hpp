@@ -710,6 +710,9 @@ TORJ_HD void fit_depo_stream_walk(const FitArgs &a, const DepoStream &ds, int i,
         depo_load(ds, a.n, i, W, C);
     else
         walk_start(W, R, C);
+    // (a form reading the next segment's five values while this one is
+    // walked spilled at three waves per SIMD and was no faster at three or two,
+    // DESIGN.md 3.4, round 5)
     walk_segments<kWalkChunkStream>(W, R, C, ja + kDepoQ);
     depo_save(ds, a.n, i, W, C);
 }
