@@ -2928,7 +2928,14 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // warm: the list of deferred (lrm > 3) points of a block (one list: the
     // alpha kernels of consecutive blocks are ordered on one stream) and one
     // counter per block
-    const int n_blk = (int)((n_steps + kb - 1) / kb);
+    // TORJ_SPLIT_FIRST: the first block's steps (a multiple of the chunk; 0 =
+    // uniform blocks): a short first block lets the alpha kernel start sooner,
+    // while the trajectory kernel alone cannot fill the chip
+    const char *first_e = getenv("TORJ_SPLIT_FIRST");
+    long first = first_e ? atol(first_e) : 0;
+    if (a.chunk_steps > 0 && first > 0) first = std::max<long>(a.chunk_steps, first - first % a.chunk_steps);
+    if (first >= kb || first >= n_steps) first = 0;
+    const int n_blk = first ? 1 + (int)((n_steps - first + kb - 1) / kb) : (int)((n_steps + kb - 1) / kb);
     const size_t b_defer = a.abs_model >= 2 ? al(4 * sizeof(unsigned long long) * n * kb) : 0,
                  b_dcnt = a.abs_model >= 2 ? al(sizeof(unsigned) * n_blk) : 0;
     const size_t bytes = R * (b_ain + b_alpha + b_awork) + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
@@ -3029,7 +3036,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const bool tile_traj = lds_env == 2, cell_traj = lds_env == 3;
     sp.traj_mode = cell_traj ? kTrajCell : tile_traj ? kTrajTile : lds_traj ? kTrajLds : kTrajL2;
     const int wpb = std::min(8, std::max(1, (G + p->n_cu - 1) / p->n_cu));
-    const int n_blocks = (int)((n_steps + kb - 1) / kb);
+    const int n_blocks = n_blk;
 #define TORJ_SPLIT_DISPATCH(K, ...)                                                         \
     do {                                                                                    \
         if (DM == kDepoSamples) {                                                           \
@@ -3044,8 +3051,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         }                                                                                   \
     } while (0)
     for (int b = 0; b < n_blocks; b++) {
-        sp.k0 = (int)(b * kb);
-        sp.kb = (int)std::min<long>(kb, n_steps - sp.k0);
+        sp.k0 = (int)(first ? (b == 0 ? 0 : first + (long)(b - 1) * kb) : b * kb);
+        sp.kb = (int)std::min<long>(first && b == 0 ? first : kb, n_steps - sp.k0);
         const int r = b % R;
         sp.ain = ain[r];
         sp.psib = psib[r];
