@@ -2877,6 +2877,17 @@ int torj_ray_entry_gpu(torj_plasma_t p, int n, const double *x0, const double *N
 
 }  // extern "C"
 
+// the reference deposition walk's per-boundary root counts, open-shell spill
+// (NaN: every shell closed) and per-ray shell powers, cleared before the walk
+// (2 GB on the headline beam: ~0.5 ms)
+static int fit_zero(const FitArgs &fa, hipStream_t st) {
+    const size_t L = (size_t)fa.n_psi, N = (size_t)fa.n;
+    HIPCK(hipMemsetAsync(fa.cnt, 0, (L + 1) * N * sizeof(int), st));
+    HIPCK(hipMemsetAsync(fa.Fopen, 0xFF, L * N * sizeof(double), st));
+    HIPCK(hipMemsetAsync(fa.dPs, 0, L * N * sizeof(double), st));
+    return 0;
+}
+
 // The split RK4 path's launches: per block of kb steps, the
 // trajectory kernel on the handle's high-priority stream, the alpha and scan
 // kernels on its low-priority one, a ring of kRing alpha-input buffers so the
@@ -3010,6 +3021,11 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     HIPCK(hipMemsetAsync(sp.sinfo, 0, b_n4, sT));
     if (dstream) HIPCK(hipMemsetAsync(ds.v + kDsJ * n, 0xFF, n * sizeof(int), sT));  // j = -1: not started
     if (dcnt) HIPCK(hipMemsetAsync(dcnt, 0, n_blk * sizeof(unsigned), s2));  // the alpha kernels' stream
+    // the walk's arrays on the scan's stream: the first window runs after the
+    // first scan there (or, for TORJ_DEPO_STREAM=2, after an event recorded
+    // there), so the clearing overlaps the first trajectory block instead of
+    // delaying it (0.5 ms per headline launch)
+    if (fa && fit_zero(*fa, s3)) return -1;
     const size_t fit_lds = fa && fa->n_psi <= kFitGridLds ? (size_t)fa->n_psi * sizeof(double) : 0;
     const int G = (int)((n + 63) / 64);
     // the trajectory kernel with the coefficients staged in LDS whenever the grid
@@ -3342,9 +3358,9 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
         fa.Fopen = (double *)(base + b_smp + b_m + b_cnt);
         fa.dPs = fa.Fopen + L * N;
         fa.kstar = (int *)(base + b_smp + b_m + b_cnt + 2 * b_fo);
-        HIPCK(hipMemsetAsync(fa.cnt, 0, (L + 1) * N * sizeof(int), s));
-        HIPCK(hipMemsetAsync(fa.Fopen, 0xFF, b_fo, s));  // NaN: every shell closed
-        HIPCK(hipMemsetAsync(fa.dPs, 0, b_fo, s));
+        // (the walk's per-boundary / per-shell arrays are cleared by fit_zero:
+        // on the split path on its scan stream, beside the first trajectory
+        // block, else on `s` before the trace)
         fa.coef = p->d_coef;
         fa.g = p->g;
         fa.n = n;
@@ -3464,6 +3480,7 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     const bool use_split = !adaptive && cfg->absorption >= 1 && cfg->n_steps > 0 &&
                            cfg->n_steps < kSplitMaxSteps &&
                            (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
+    if (fit && !use_split && fit_zero(fa, s)) return -1;
     if (use_split) {
         if (split_trace(p, a, DM, tr, cs, s, fit ? &fa : nullptr, &dstr)) return -1;
     } else if (use_sched && cfg->n_steps > 0) {
