@@ -1,3 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-timeout -k 10 900 bash scripts/gpu_ab.sh g13 base tw3 aw6 base tw3 aw6 || exit 1
+O=gpurun_out/g23; mkdir -p $O
+timeout -k 10 600 bash scripts/gpu_ab.sh g23 prevsum base prevsum base || exit 1
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu -k "deposition or c3 or beam" --timeout 600 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -3 $O/pytest.log
