@@ -1303,7 +1303,7 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
         }
     }
 #endif
-    const double Nabs = sqrt_pos(N2), Te = exp_fast(lnTe);
+    const double Nabs = sqrt_pos(N2), Te = exp_fast<true>(lnTe);
     if constexpr (COUNT) {
         AlbajarWork work = {};
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
@@ -2203,6 +2203,23 @@ static int ensure_fit(torj_plasma_s *p, size_t bytes) {
     return 0;
 }
 
+// a split-pipeline stream's priority: `dflt`, or the environment's value clamped
+// to the device's range (measurement knobs: TORJ_ALPHA_PRIO, TORJ_SCAN_PRIO,
+// TORJ_DEPO_PRIO; TORJ_PRIO_VERBOSE=1 prints the range)
+static int stream_prio(const char *name, int lo, int hi) {
+    static const bool verbose = [&] {
+        const char *v = getenv("TORJ_PRIO_VERBOSE");
+        const bool on = v && atoi(v) != 0;
+        if (on) fprintf(stderr, "torj: stream priority range least %d greatest %d\n", lo, hi);
+        return on;
+    }();
+    const char *e = getenv(name);
+    int v = lo;
+    if (e) v = std::min(std::max(atoi(e), std::min(lo, hi)), std::max(lo, hi));
+    if (verbose) fprintf(stderr, "torj: %s -> %d\n", name, v);
+    return v;
+}
+
 static int ensure_split(torj_plasma_s *p, size_t bytes) {
     std::lock_guard<std::mutex> lk(p->mu);
     if (!p->stream2) {
@@ -2237,8 +2254,8 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
             HIPCK(hipExtStreamCreateWithCUMask(&p->streamS, (uint32_t)mA.size(), mA.data()));
         } else {
             HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
-            HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, lo));
-            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, lo));
+            HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, stream_prio("TORJ_ALPHA_PRIO", lo, hi)));
+            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, stream_prio("TORJ_SCAN_PRIO", lo, hi)));
         }
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
@@ -2943,7 +2960,8 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     // =2: on a stream of their own, each after its block's scan, so the next
     // scan (and the ring slot it releases) does not wait behind them; =3: on
     // the scan's stream, each window's elimination and walk as two launches
-    // (the default since round 4: DESIGN.md 3.4)
+    // (the default since round 4: DESIGN.md 3.4); =4: the two launches on a
+    // stream of their own (as 2)
     const char *dstream_e = getenv("TORJ_DEPO_STREAM");  // read per call (tests compare both)
     const int dstream_env = dstream_e ? atoi(dstream_e) : 3;
     const bool dstream = fa && dso && dstream_env != 0;
@@ -3016,11 +3034,11 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     }();
     hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
     hipStream_t s3 = serial ? s : (scan_own ? p->streamS : p->stream2);
-    const bool depo_own = dstream && dstream_env == 2 && !serial;
+    const bool depo_own = dstream && (dstream_env == 2 || dstream_env == 4) && !serial;
     if (depo_own && !p->streamD) {  // created on first use only: one more queue otherwise
         int lo = 0, hi = 0;
         HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, lo));
+        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, stream_prio("TORJ_DEPO_PRIO", lo, hi)));
     }
     hipStream_t sD = depo_own ? p->streamD : s3;
     if (!serial) {  // fork from the caller's stream
@@ -3135,7 +3153,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         // behind the alpha or the trajectory kernel's stream 3.03 / 2.98e9)
         if (dstream && b + 1 < n_blocks) {
             if (depo_own) HIPCK(hipStreamWaitEvent(sD, p->ev_S[r], 0));
-            if (dstream_env == 3) {  // elimination and walk as two launches
+            if (dstream_env == 3 || dstream_env == 4) {  // elimination and walk as two launches
                 hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sD, *fa, ds, sp.sinfo, sp.k0 + sp.kb);
                 hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
                                    sp.k0 + sp.kb);

@@ -154,6 +154,26 @@ TORJ_HD double sqrt_node(double x) {
 // ldexp (~1 ulp).  No special-case paths: ldexp overflows to inf above ~709
 // and underflows to 0 below ~-745, NaN stays NaN.  Used for n_e, T_e from
 // their log splines (the node loop takes exp2_node below).
+// A constant for a VALU operand, materialised in an SGPR pair at its use
+// (exp_fast<true>): left to itself the compiler puts a straight-line Horner
+// chain's coefficients in VGPRs, two v_mov_b32 per coefficient ahead of a
+// v_fmac -- 20 VALU of exp_fast's 37 -- where two s_mov_b32 and a v_fma_f64
+// with an SGPR operand do.  The empty asm is volatile so that it is neither
+// hoisted nor merged: the pair lives for one instruction.  For kernels with
+// SGPRs to spare only (k_alpha_pts: 103 of 106, no spills); the trajectory
+// kernel, at 106 with spills, keeps its constants hoisted in VGPRs.
+#ifndef TORJ_EXP_SCONST
+#define TORJ_EXP_SCONST 1
+#endif
+template <bool S>
+TORJ_HD double poly_c(double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if constexpr (S && TORJ_EXP_SCONST) asm volatile("" : "+s"(c));
+#endif
+    return c;
+}
+
+template <bool SC = false>
 TORJ_HD double exp_fast(double x) {
 #if defined(__HIP_DEVICE_COMPILE__)
     const double k = __builtin_rint(x * 1.4426950408889634074);
@@ -161,16 +181,16 @@ TORJ_HD double exp_fast(double x) {
     r = fma(-k, 2.31904681384629955842e-17, r);
     // degree 11 near-minimax on |r| <= ln2/2 (tools/gen_exp_poly.py: 0.58 ulp,
     // against 1.5 ulp for the degree 12 Taylor polynomial)
-    double p = 2.5100375832561234e-08;
-    p = fma(p, r, 2.7620075879983367e-07);
-    p = fma(p, r, 2.7557268480310024e-06);
-    p = fma(p, r, 2.4801521322368692e-05);
-    p = fma(p, r, 0.00019841269863040545);
-    p = fma(p, r, 0.0013888888917196719);
-    p = fma(p, r, 0.008333333333330065);
-    p = fma(p, r, 0.041666666666624164);
-    p = fma(p, r, 0.16666666666666669);
-    p = fma(p, r, 0.5000000000000001);
+    double p = poly_c<SC>(2.5100375832561234e-08);
+    p = fma(p, r, poly_c<SC>(2.7620075879983367e-07));
+    p = fma(p, r, poly_c<SC>(2.7557268480310024e-06));
+    p = fma(p, r, poly_c<SC>(2.4801521322368692e-05));
+    p = fma(p, r, poly_c<SC>(0.00019841269863040545));
+    p = fma(p, r, poly_c<SC>(0.0013888888917196719));
+    p = fma(p, r, poly_c<SC>(0.008333333333330065));
+    p = fma(p, r, poly_c<SC>(0.041666666666624164));
+    p = fma(p, r, poly_c<SC>(0.16666666666666669));
+    p = fma(p, r, poly_c<SC>(0.5000000000000001));
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
     // v_cvt_i32_f64 saturates out-of-range k (the C conversion would be UB),
@@ -1231,7 +1251,7 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
 #pragma unroll
         for (int k = 1; k < 2 * M - 1; k++) p *= hx;
         const double R = (4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax)) * rcp_nz(fabs(dom));
-        const double Emax = exp_fast(mu * (1.0 - sqrt_nn(qmin)));
+        const double Emax = exp_fast<true>(mu * (1.0 - sqrt_nn(qmin)));
         // R < 1e300: an E_max that underflowed to 0 cannot hide a huge R
         if (R < 1e300 && R * Emax < 0x1p-58) {
             if (work) work->n_negl++;
