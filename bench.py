@@ -43,9 +43,10 @@ SPLIT_KERNELS = "k_traj|k_alpha_pts|k_tau_scan|k_split_final"
 # version of the FLOP model behind roofline.achieved (torj_hip/flops.py); bumped
 # whenever a counter's meaning or a per-unit price changes, so figures of
 # different rounds are compared only under the same model
-FLOP_MODEL = {"albajar": "albajar-v3 (round 3: exact-zero, negligible and settled-early "
-                         "harmonics priced at their tests)",
-              "none": "albajar-v3",
+FLOP_MODEL = {"albajar": "albajar-v4 (round 5: harmonics skipped below tiny_alpha = 1e-20 m^-1 priced as "
+                         "negligible ones; round 3: exact-zero, negligible and settled-early harmonics "
+                         "priced at their tests)",
+              "none": "albajar-v4",
               "warm_wr": "warm-v3 (round 5: warmdisp's breaking pass sums no tensor, its root by "
                          "the conjugate product, the asymptotic Faddeeva series by Horner; round 3: counter[2] = asymptotic Faddeeva "
                          "evaluations; larmornumber tests priced at one per call, a lower bound)"}
@@ -882,6 +883,10 @@ def _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads):
               "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
               "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
               "max_rel_tau_unfloored": float(et_strict.max()),
+              # below the floor the bar is absolute: the largest |tau_gpu - tau_cpu| there
+              # (the tiny-alpha skip moves tau by < 2e-20 per metre of ray)
+              "max_abs_tau_below_floor": float(np.where(np.abs(os_[:, 6]) < 1e-6,
+                                                        np.abs(gs[:, 6] - os_[:, 6]), 0.0).max()),
               "max_rel": float(max(ex.max(), eN.max(), et.max())),
               "rays_within_bar": int((np.maximum(np.maximum(ex, eN), et)
                                       <= {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10)).sum()),

@@ -320,7 +320,8 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
         return cnt.cpu().numpy()
 
     res, cnts = {}, {}
-    old = os.environ.get("TORJ_NEGL_SKIP")
+    old = os.environ.get("TORJ_NEGL_SKIP"), os.environ.get("TORJ_TINY_ALPHA")
+    os.environ["TORJ_TINY_ALPHA"] = "0"  # the bounded tiny-alpha skip off: bit-identity holds
     try:
         for skip in ("0", "1"):
             os.environ["TORJ_NEGL_SKIP"] = skip
@@ -329,10 +330,11 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
                 res[skip, sched] = _run(T, hplasma, sched, 0, xp, Np, om, 1, **kw)
                 cnts[skip, sched] = counters(sched)
     finally:
-        if old is None:
-            os.environ.pop("TORJ_NEGL_SKIP", None)
-        else:
-            os.environ["TORJ_NEGL_SKIP"] = old
+        for k, v in zip(("TORJ_NEGL_SKIP", "TORJ_TINY_ALPHA"), old):
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         T.abs_Al_init(24)
     for sched in (3, 0):
         a, b = res["0", sched], res["1", sched]
@@ -347,6 +349,77 @@ def test_negligible_harmonic_skip_bit_identical(gpu, T, hplasma):
         assert c0[7] == 0 and c1[7] > 0 and c1[2] < c0[2] and c1[5] < c0[5], (c0, c1)
         assert c1[5] + c1[7] >= c0[5], (c0, c1)
     assert np.array_equal(cnts["1", 3], cnts["1", 0])
+
+
+def _trace_counted(T, hplasma, sched, xp, Np, om):
+    """One traced launch's work counters (torj_trace_device with a counters array)."""
+    import ctypes
+
+    import torch
+
+    n = len(xp)
+    dev = torch.device("cuda", 0)
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    x0, N0 = t(xp.T), t(Np.T)
+    state = torch.empty((7, n), dtype=torch.float64, device=dev)
+    st = torch.empty(n, dtype=torch.int32, device=dev)
+    k = torch.empty(n, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(8, dtype=torch.int64, device=dev)
+    cfg = T._lib.TraceCfg(om, 1, 1e-4, 2000, 20, 1.0, 1e-6, 1, 0)
+    stream = torch.cuda.current_stream(dev)
+    hplasma.set_sched(sched, 0)
+    try:
+        T._lib.check(T.lib().torj_trace_device(hplasma.handle, cfg, n, x0.data_ptr(), N0.data_ptr(),
+                                               None, 0, None, state.data_ptr(), st.data_ptr(),
+                                               k.data_ptr(), None, None, None,
+                                               ctypes.c_void_p(cnt.data_ptr()), stream.cuda_stream))
+        T._lib.check(T.lib().torj_trace_check(hplasma.handle, stream.cuda_stream))
+    finally:
+        hplasma.set_sched(-1)
+    return cnt.cpu().numpy()
+
+
+@pytest.mark.parametrize("sched", [3, 0])
+def test_tiny_alpha_skip_bounded(gpu, T, hplasma, sched):
+    """The skip of harmonic integrals whose share of alpha is provably below
+    tiny_alpha (torj_math.hpp albajar_harmonic / tiny_harmonic; default 1e-20
+    m^-1, TORJ_TINY_ALPHA=0 evaluates every integral): on the split pipeline and
+    the fused kernel, statuses, steps and trajectories are bit-identical, tau
+    moves by at most 2 tiny_alpha per metre of ray (two harmonics) plus the
+    rounding of the sums the skipped terms left, the deposited power likewise;
+    the skip fires (counter [6] up, counter [3] down by as much)."""
+    import os
+
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=2000, weights=w, traj_stride=100, psi_grid=np.linspace(0, 1, 1000),
+              deposition="reference", x_launch=pos, s0=s0)
+    res, cnts = {}, {}
+    old = os.environ.get("TORJ_TINY_ALPHA")
+    try:
+        for tiny in ("0", "1e-20"):
+            os.environ["TORJ_TINY_ALPHA"] = tiny
+            T.abs_Al_init(24)
+            res[tiny] = _run(T, hplasma, sched, 0, xp, Np, om, 1, **kw)
+            cnts[tiny] = _trace_counted(T, hplasma, sched, xp, Np, om)
+    finally:
+        if old is None:
+            os.environ.pop("TORJ_TINY_ALPHA", None)
+        else:
+            os.environ["TORJ_TINY_ALPHA"] = old
+        T.abs_Al_init(24)
+    a, b = res["0"], res["1e-20"]
+    for f in ("status", "steps"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.array_equal(a.state[:, :6], b.state[:, :6])
+    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    L = a.steps * 1e-4  # metres of ray traced
+    dtau = np.abs(a.state[:, 6] - b.state[:, 6])
+    assert (dtau <= 2 * 1e-20 * L + 4e-16 * np.abs(a.state[:, 6])).all(), dtau.max()
+    assert np.abs(a.P_dep - b.P_dep).max() <= 1e-12
+    assert np.abs(a.dP_shell - b.dP_shell).max() <= 1e-12 * np.abs(a.dP_shell).max()
+    c0, c1 = cnts["0"], cnts["1e-20"]
+    assert np.array_equal(c0[[0, 1, 2, 5, 7]], c1[[0, 1, 2, 5, 7]]), (c0, c1)
+    assert c1[6] > c0[6] and c1[3] + c1[6] == c0[3] + c0[6], (c0, c1)
 
 
 def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):

@@ -1276,7 +1276,7 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArg
 constexpr int kAlphaBlock = TORJ_ALPHA_BLOCK;
 template <bool COUNT>
 __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
-    const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
+    const int q = blockIdx.x, js = blockIdx.y;  // js = j * 4 + stage (a 2-D grid: no division)
     const int i = q * kAlphaBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
@@ -1307,13 +1307,13 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     if constexpr (COUNT) {
         AlbajarWork work = {};
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, &work);
+            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, &work, 0, c_gl.tiny_alpha);
         sp.awork[(size_t)js * a.n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
                                      ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
                                      ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
     } else {
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
-            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, nullptr);
+            c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, nullptr, 0, c_gl.tiny_alpha);
     }
 }
 
@@ -1346,7 +1346,7 @@ __device__ __forceinline__ void warm_store(const SplitArgs &sp, int js, int i, i
 template <int IWARM, bool COUNT>
 __global__ void __launch_bounds__(kAlphaWarmBlock, IWARM == 1 ? TORJ_WARM1_ALPHA_WAVES : TORJ_WARM3_ALPHA_WAVES)
     k_alpha_warm_pts(TraceArgs a, SplitArgs sp, int nq) {
-    const int q = blockIdx.x % nq, js = blockIdx.x / nq;  // js = j * 4 + stage
+    const int q = blockIdx.x, js = blockIdx.y;  // js = j * 4 + stage
     const int i = q * kAlphaWarmBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
@@ -2452,6 +2452,16 @@ int torj_abs_al_init(int n) {
     // and the test that holds both bit-identical), read at each abs_Al_init
     const char *ne = getenv("TORJ_NEGL_SKIP");
     t.negl_skip = ne ? (atoi(ne) != 0) : 1;
+    // the bounded skip of a harmonic whose share of alpha is provably below
+    // tiny_alpha m^-1 (albajar_harmonic; ray tracing only -- the point entry
+    // torj_abs_albajar_fast evaluates every harmonic): tau moves by less than
+    // 2 tiny_alpha per metre of ray, 4e-21 on the headline rays, against the
+    // parity bar's 1e-16 absolute floor (C3 trace phase 45.1 -> 40.7 ms, DESIGN.md
+    // 3.7).  Env TORJ_TINY_ALPHA overrides (0 = off: every integral evaluated),
+    // read at each abs_Al_init
+    const char *ta = getenv("TORJ_TINY_ALPHA");
+    t.tiny_alpha = ta ? atof(ta) : kTinyAlpha;
+    if (!(t.tiny_alpha >= 0.0 && t.tiny_alpha < 1e-12)) return fail("TORJ_TINY_ALPHA=%s outside [0, 1e-12)", ta);
     gauss_legendre(n, t.t, t.w);
     for (int i = 0; i < n; i++) {
         t.st[i] = std::sqrt(1.0 - t.t[i] * t.t[i]);
@@ -2943,8 +2953,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int nf = a.abs_model >= 2 ? kAinFW : kAinF;
     const size_t per_step = 4 * (size_t)nf * sizeof(double) * n;
     long kb = (long)std::max<size_t>(1, budget / per_step);
+    kb = std::min<long>(kb, 16383);  // the alpha kernels' grid.y = 4 kb stays <= 65535
     if (a.chunk_steps > 0 && kb >= a.chunk_steps) kb -= kb % a.chunk_steps;
-    if (p->sched_mode == 3 && p->sched_waves > 0) kb = p->sched_waves;  // torj_set_sched(p, 3, steps per block)
+    if (p->sched_mode == 3 && p->sched_waves > 0) kb = std::min(p->sched_waves, 16383);  // torj_set_sched(p, 3, steps per block)
     kb = std::min<long>(kb, n_steps);
     const int n_cb = (a.chunk_steps > 0 ? n_steps / a.chunk_steps : 0) + 1;
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -3118,9 +3129,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         HIPCK(hipEventRecord(p->ev_T[r], sT));
         HIPCK(hipStreamWaitEvent(s2, p->ev_T[r], 0));
         const int nqA = (int)((n + kAlphaBlock - 1) / kAlphaBlock);
-        const dim3 agridA((unsigned)(nqA * 4 * sp.kb));
+        const dim3 agridA((unsigned)nqA, (unsigned)(4 * sp.kb));  // ray groups fastest
         const int nqW = (int)((n + kAlphaWarmBlock - 1) / kAlphaWarmBlock);
-        const dim3 agridW((unsigned)(nqW * 4 * sp.kb));
+        const dim3 agridW((unsigned)nqW, (unsigned)(4 * sp.kb));
         sp.defer_cnt = dcnt ? dcnt + b : nullptr;
 #define TORJ_WARM_LAUNCH(IW, C)                                                                     \
     do {                                                                                            \

@@ -887,9 +887,12 @@ constexpr double inv_fact(int k) {
 // c_nu[k] = 1/(k! (k+nu)!) : S_nu(z) = sum_k c_nu[k] z^k, J_nu(x) = (x/2)^nu S_nu(-x^2/4)
 constexpr double series_coef(int nu, int k) { return inv_fact(k) * inv_fact(k + nu); }
 
+// the default of GLTable::tiny_alpha (m^-1; torj_abs_al_init, TORJ_TINY_ALPHA)
+constexpr double kTinyAlpha = 1e-20;
 struct GLTable {
     int n;
     int negl_skip;  // 1: skip harmonic integrals provably below an ulp of the sum (default)
+    double tiny_alpha;  // > 0: skip a harmonic whose rigorous bound on |alpha| is below it (m^-1)
     double t[kMaxGL], w[kMaxGL], st[kMaxGL], t2[kMaxGL];  // nodes, weights, sqrt(1-t^2), t^2
     // the node loop's per-node constants (pair_term), per harmonic m, one
     // 32-byte record per node (one scalar load of 8 dwords per pair): t, t^2,
@@ -1187,7 +1190,7 @@ template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg,
                                 double inv_sqNp, double N_perp, double omega_bar,
                                 double Axz, double ea, double e3, AlbajarWork *work, int sub = 0,
-                                double dom = 0.0) {
+                                double dom = 0.0, double hmax = 0.0) {
     constexpr double md = (double)M, inv_md = 1.0 / md;
     HarmConst c;
     c.r2m1 = hg.r2m1;
@@ -1240,7 +1243,15 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     // every node's E <= E_max = exp(mu (1 - gamma_min)) and sum_i w_i = 2,
     // |node sum| <= 4 E_max hx^(2m-1) (Pmax + Qmax).  The level ballot above
     // already counted this lane, so the other lanes' polynomials do not change.
-    if (gl.negl_skip && dom != 0.0 && fabs(dom) < INFINITY && fabs(dom) > 1e-290) {
+    //
+    // Below any absorption a result can show (hmax > 0, GLTable::tiny_alpha):
+    // the same bound B E_max on |this integral|, times the normalisation
+    // albajar_finish applies, is an upper bound on the harmonic's share of
+    // alpha; when it is below tiny_alpha (m^-1) the node loop is skipped.  Not
+    // bit-identical: alpha moves by less than tiny_alpha per skipped harmonic,
+    // tau by less than 2 tiny_alpha per metre of ray.
+    const bool rel = gl.negl_skip && dom != 0.0 && fabs(dom) < INFINITY && fabs(dom) > 1e-290;
+    if (rel || hmax > 0.0) {
         constexpr double iS = inv_fact(M), iS1 = inv_fact(M + 1), iSl = inv_fact(M - 1);
         const double hx = c.hx, hx2 = hx * hx;
         const double A = hx * (iS * iS), T1 = hx2 * iS1;
@@ -1250,10 +1261,11 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
         double p = hx;  // hx^(2m-1)
 #pragma unroll
         for (int k = 1; k < 2 * M - 1; k++) p *= hx;
-        const double R = (4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax)) * rcp_nz(fabs(dom));
+        const double B0 = 4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax);
+        const double R = B0 * rcp_nz(fabs(dom));
         const double Emax = exp_fast<true>(mu * (1.0 - sqrt_nn(qmin)));
-        // R < 1e300: an E_max that underflowed to 0 cannot hide a huge R
-        if (R < 1e300 && R * Emax < 0x1p-58) {
+        // R, B0 < 1e300: an E_max that underflowed to 0 cannot hide a huge bound
+        if ((rel && R < 1e300 && R * Emax < 0x1p-58) || (B0 < 1e300 && B0 * Emax < hmax)) {
             if (work) work->n_negl++;
             return 0.0;
         }
@@ -1397,10 +1409,11 @@ TORJ_HD AlbPro albajar_prologue(const AlbPre &pre, double X, double Y, double N_
 // harmonic, as the reference's `m < m_0` test makes it)
 template <int M, int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double albajar_pro_harmonic(const GLTable &gl, const AlbPro &q, const HarmGeom &hg,
-                                    AlbajarWork *work, int sub = 0, double dom = 0.0) {
+                                    AlbajarWork *work, int sub = 0, double dom = 0.0,
+                                    double hmax = 0.0) {
     const uint32_t z0 = work ? work->n_zero + work->n_negl : 0u;
     const double h = albajar_harmonic<M, LPR, U>(gl, q.mu, hg, q.inv_sqNp, q.N_perp, q.omega_bar,
-                                                 q.Axz, q.ea, q.e3, work, sub, dom);
+                                                 q.Axz, q.ea, q.e3, work, sub, dom, hmax);
     if (work && work->n_zero + work->n_negl == z0) work->n_harm++;
     return h;
 }
@@ -1415,10 +1428,23 @@ TORJ_HD double albajar_finish(const AlbPro &q, double c_abs, double X, double om
     return c_abs * X * omega * (q.omega_bar * (1.0 / kC));
 }
 
+// The largest harmonic integral (albajar_harmonic's units) whose share of alpha
+// is provably below gl.tiny_alpha: tiny_alpha over an upper bound on the
+// normalisation albajar_finish multiplies the sum by (its a <= 1 for mu > 0,
+// (mu / 2 pi)^1.5 from a reciprocal square root, and a factor 1/2 for the
+// roundings of this bound); 0 (no skip) when off or not finite.
+TORJ_HD double tiny_harmonic(double tiny_alpha, const AlbPro &q, double X, double omega) {
+    if (!(tiny_alpha > 0.0)) return 0.0;
+    const double m = q.mu * (1.0 / (2.0 * kPi));
+    const double F = fabs((2.0 * kPi * kPi) * q.inv_m0 * X * omega * (q.omega_bar * (1.0 / kC)) * m);
+    const double h = 0.5 * tiny_alpha * rcp_nz(F) * rsqrt_pos(m);
+    return h < INFINITY ? h : 0.0;
+}
+
 template <int LPR = 1, int U = TORJ_PAIR_UNROLL>
 TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, double Y,
                                      double N_abs, double N_par, double Te, int mode,
-                                     AlbajarWork *work, int sub = 0) {
+                                     AlbajarWork *work, int sub = 0, double tiny = 0.0) {
     if (Te < 20.0) return 0.0;
     const AlbPre pre = albajar_pre(Y, N_abs, N_par, Te);
     const bool h2 = !(2.0 < pre.m_0), h3 = !(3.0 < pre.m_0);  // harmonic m present iff m >= m_0
@@ -1442,17 +1468,19 @@ TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, 
     const AlbPro q = albajar_prologue(pre, X, Y, N_abs, N_par, mode);
     if (!q.ok) return 0.0;
     if (work) work->n_active++;
+    const double hmax = tiny_harmonic(tiny, q, X, omega);
     double c_abs = 0.0;
-    if (h2) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, g2, work, sub);
-    if (h3) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, g3, work, sub, c_abs);
+    if (h2) c_abs += albajar_pro_harmonic<2, LPR, U>(gl, q, g2, work, sub, 0.0, hmax);
+    if (h3) c_abs += albajar_pro_harmonic<3, LPR, U>(gl, q, g3, work, sub, c_abs, hmax);
     return albajar_finish(q, c_abs, X, omega);
 }
 // the fused trace kernels' call (out of line there, see TORJ_ALB_ATTR); kernels
 // with nothing else to hold (the split path's alpha kernel) inline the body
 template <int LPR = 1>
 TORJ_ALB_ATTR double abs_albajar_fast(const GLTable &gl, double omega, double X, double Y, double N_abs,
-                                double N_par, double Te, int mode, AlbajarWork *work, int sub = 0) {
-    return abs_albajar_fast_body<LPR>(gl, omega, X, Y, N_abs, N_par, Te, mode, work, sub);
+                                double N_par, double Te, int mode, AlbajarWork *work, int sub = 0,
+                                double tiny = 0.0) {
+    return abs_albajar_fast_body<LPR>(gl, omega, X, Y, N_abs, N_par, Te, mode, work, sub, tiny);
 }
 
 // one RHS evaluation of sys! (src/solve.jl:112-114 -> gradΛ!, :85-95)
@@ -1466,7 +1494,7 @@ TORJ_HD void ray_rhs(const double *__restrict__ coef, const Grid &g, const Const
     dispersion_grad(p, N, mode, du, &Npar);
     if constexpr (ABS) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work);
+        alpha = abs_albajar_fast(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, 0, gl.tiny_alpha);
     } else {
         alpha = 0.0;
     }

@@ -1151,7 +1151,8 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
     dispersion_grad(p, N, mode, du, &Npar, &inv);
     if constexpr (ABS == 1) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
-        alpha = abs_albajar_fast<LPR>(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, sub);
+        alpha = abs_albajar_fast<LPR>(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, sub,
+                                      gl.tiny_alpha);
     } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         const WarmAlpha r =
