@@ -74,7 +74,9 @@ def test_c3_fan_reference_deposition_vs_fitpack(c3, oplasma):
         sv, psi, dpds = D.ray_vectors(c3["pos"][i], c3["s0"][i], DS, o["steps"][k],
                                       o["samples"][k], oplasma.evaluate("psi", c3["pos"][i]))
         _, P = D.power_deposition_profile(sv, psi, dpds, c3["grid"], oplasma.volume)
-        assert abs(g.P_dep[i] - P) <= 1e-11 * max(P, 1e-300), (i, g.P_dep[i], P)
+        # + the tiny-alpha skip's bound: alpha moves by < 1e-20 m^-1 per
+        # harmonic, so the ray's deposited power by < 2e-20 per metre traced
+        assert abs(g.P_dep[i] - P) <= 1e-11 * P + 2e-20 * DS * o["steps"][k], (i, g.P_dep[i], P)
 
 
 def _close(a, b, tol, tau_floor=1e-13):

@@ -411,8 +411,13 @@ def test_tiny_alpha_skip_bounded(gpu, T, hplasma, sched):
     for f in ("status", "steps"):
         assert np.array_equal(getattr(a, f), getattr(b, f)), f
     assert np.array_equal(a.state[:, :6], b.state[:, :6])
-    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    # trajectory samples (n, n_save, 5): x, y, z and s bit-identical, tau as tau
+    rows = [0, 1, 2, 4]
+    assert np.array_equal(a.traj[:, :, rows], b.traj[:, :, rows], equal_nan=True)
+    assert np.array_equal(np.isfinite(a.traj[:, :, 3]), np.isfinite(b.traj[:, :, 3]))
+    fin = np.isfinite(a.traj[:, :, 3])
     L = a.steps * 1e-4  # metres of ray traced
+    assert (np.abs(a.traj[:, :, 3] - b.traj[:, :, 3])[fin] <= 2e-20 * 0.2 + 4e-16 * np.abs(a.traj[:, :, 3])[fin]).all()
     dtau = np.abs(a.state[:, 6] - b.state[:, 6])
     assert (dtau <= 2 * 1e-20 * L + 4e-16 * np.abs(a.state[:, 6])).all(), dtau.max()
     assert np.abs(a.P_dep - b.P_dep).max() <= 1e-12

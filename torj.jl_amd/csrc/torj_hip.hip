@@ -465,7 +465,7 @@ template <int ABS>
 __device__ __forceinline__ void rhs7(const TraceArgs &a, const double u[7], double du[7],
                                      AlbajarWork &work, unsigned long long &nrhs) {
     double al;
-    ray_rhs_m<ABS>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, a.abs_model, u, u + 3, du, al, &work);
+    ray_rhs_m<ABS, 1, false>(a.coef, a.g, a.k, c_gl, a.omega, a.mode, a.abs_model, u, u + 3, du, al, &work);
     du[6] = -u[6] * al;  // sys!: du[7] = -P alpha (src/solve.jl:113)
     nrhs++;
 }
@@ -1040,6 +1040,9 @@ __device__ __forceinline__ int cell_index(double x, double x1, double xn, double
     return i < 0 ? 0 : (i > n - 2 ? n - 2 : i);
 }
 
+#ifndef TORJ_TRAJ_PREWAIT
+#define TORJ_TRAJ_PREWAIT 1
+#endif
 // the trajectory steps of one ray over the block, from its carry (x, N, steps)
 template <int DEPO, bool TRAJ, int NS, class CS>
 __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp, CS coef, int i,
@@ -1071,6 +1074,13 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
     };
     const int s_first = steps;
     bool pending = false;  // step steps - 1 still needs its psi
+#if defined(__HIP_DEVICE_COMPILE__) && TORJ_TRAJ_PREWAIT
+    // every load before the step loop complete here (s_waitcnt vmcnt(0)): the
+    // compiler otherwise waits at the loop header for the carry's loads, every
+    // step, and on gfx9 vmcnt counts stores too -- each step would then wait for
+    // its own last stage's alpha-input stores to reach memory
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
     for (int s = s_first; s < s_end; s++) {
         double xn[3], Nn[3], psi_x;
         const bool bad = cold_step<true, NS, CS, true>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn, &psi_x);
@@ -1274,8 +1284,14 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArg
 // trace phase, 128: 45.6-45.7, 64: 46.7-48.6 alternating)
 #endif
 constexpr int kAlphaBlock = TORJ_ALPHA_BLOCK;
+#ifndef TORJ_ALPHA_SETPRIO
+#define TORJ_ALPHA_SETPRIO 0
+#endif
 template <bool COUNT>
 __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(TraceArgs a, SplitArgs sp, int nq) {
+#if TORJ_ALPHA_SETPRIO
+    __builtin_amdgcn_s_setprio(TORJ_ALPHA_SETPRIO);  // measurement knob: the alpha waves' issue priority
+#endif
     const int q = blockIdx.x, js = blockIdx.y;  // js = j * 4 + stage (a 2-D grid: no division)
     const int i = q * kAlphaBlock + threadIdx.x;
     if (i >= a.n) return;
@@ -2204,9 +2220,9 @@ static int ensure_fit(torj_plasma_s *p, size_t bytes) {
 }
 
 // a split-pipeline stream's priority: `dflt`, or the environment's value clamped
-// to the device's range (measurement knobs: TORJ_ALPHA_PRIO, TORJ_SCAN_PRIO,
-// TORJ_DEPO_PRIO; TORJ_PRIO_VERBOSE=1 prints the range)
-static int stream_prio(const char *name, int lo, int hi) {
+// to the device's range (measurement knobs: TORJ_TRAJ_PRIO, TORJ_ALPHA_PRIO,
+// TORJ_SCAN_PRIO, TORJ_DEPO_PRIO; TORJ_PRIO_VERBOSE=1 prints the range)
+static int stream_prio(const char *name, int dflt, int lo, int hi) {
     static const bool verbose = [&] {
         const char *v = getenv("TORJ_PRIO_VERBOSE");
         const bool on = v && atoi(v) != 0;
@@ -2214,7 +2230,7 @@ static int stream_prio(const char *name, int lo, int hi) {
         return on;
     }();
     const char *e = getenv(name);
-    int v = lo;
+    int v = dflt;
     if (e) v = std::min(std::max(atoi(e), std::min(lo, hi)), std::max(lo, hi));
     if (verbose) fprintf(stderr, "torj: %s -> %d\n", name, v);
     return v;
@@ -2253,9 +2269,9 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
             HIPCK(hipExtStreamCreateWithCUMask(&p->stream2, (uint32_t)mA.size(), mA.data()));
             HIPCK(hipExtStreamCreateWithCUMask(&p->streamS, (uint32_t)mA.size(), mA.data()));
         } else {
-            HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, hi));
-            HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, stream_prio("TORJ_ALPHA_PRIO", lo, hi)));
-            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, stream_prio("TORJ_SCAN_PRIO", lo, hi)));
+            HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, stream_prio("TORJ_TRAJ_PRIO", hi, lo, hi)));
+            HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, stream_prio("TORJ_ALPHA_PRIO", lo, lo, hi)));
+            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, stream_prio("TORJ_SCAN_PRIO", lo, lo, hi)));
         }
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
@@ -3049,7 +3065,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     if (depo_own && !p->streamD) {  // created on first use only: one more queue otherwise
         int lo = 0, hi = 0;
         HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, stream_prio("TORJ_DEPO_PRIO", lo, hi)));
+        HIPCK(hipStreamCreateWithPriority(&p->streamD, hipStreamNonBlocking, stream_prio("TORJ_DEPO_PRIO", lo, lo, hi)));
     }
     hipStream_t sD = depo_own ? p->streamD : s3;
     if (!serial) {  // fork from the caller's stream

@@ -1140,7 +1140,10 @@ TORJ_HD double alpha_warm(double omega, double X, double Y, double N_abs, double
 // one RHS evaluation: ABS 0 cold, 1 Albajar (abs_Albajar_fast), 2 warm weakly
 // relativistic (iwarm 1), 3 warm fully relativistic (iwarm 3); separate
 // instances keep each model's registers and private frame out of the others
-template <int ABS, int LPR = 1>
+// TINY: the Albajar model's bounded tiny-alpha skip (GLTable::tiny_alpha) on
+// (fixed-step RK4); the adaptive integrator evaluates every integral, so that
+// its step control sees the exact alpha
+template <int ABS, int LPR = 1, bool TINY = true>
 TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Consts &k,
                        const GLTable &gl, double omega, int mode, int model, const double x[3],
                        const double N[3], double du[6], double &alpha, AlbajarWork *work,
@@ -1152,7 +1155,7 @@ TORJ_HD void ray_rhs_m(const double *__restrict__ coef, const Grid &g, const Con
     if constexpr (ABS == 1) {
         const double Nabs = sqrt_pos(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         alpha = abs_albajar_fast<LPR>(gl, omega, p.X, p.Y, Nabs, Npar, exp_fast(p.lnTe), mode, work, sub,
-                                      gl.tiny_alpha);
+                                      TINY ? gl.tiny_alpha : 0.0);
     } else if constexpr (ABS >= 2) {
         const double Nabs = sqrt(N[0] * N[0] + N[1] * N[1] + N[2] * N[2]);
         const WarmAlpha r =
