@@ -917,6 +917,9 @@ __device__ __forceinline__ int info_steps(int v) { return v & 0xffffff; }
 __device__ __forceinline__ int info_status(int v) { return (unsigned)v >> 24; }
 __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st << 24); }
 
+#ifndef TORJ_AIN_TRAJ_MATH  // 1: the trajectory kernel stores |N| and Te for k_alpha_pts (not |N|^2, ln Te)
+#define TORJ_AIN_TRAJ_MATH 0
+#endif
 // One cold RK4 step of ray_segment's arithmetic (plasma_point with ln Te, as
 // the absorbing kernels evaluate it); STORE: this step's alpha inputs -> ain.
 // PSI: stage 0's stencil also sums psi at x (the step's start), returned in
@@ -961,6 +964,12 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
                 o[2 * (size_t)a.n] = sqrt(N2);
                 o[4 * (size_t)a.n] = exp(p.lnTe);
                 o[kAinF * (size_t)a.n] = inv;
+            } else if constexpr (TORJ_AIN_TRAJ_MATH) {
+                // |N| and Te by the functions k_alpha_pts would apply (the same
+                // bits), on the trajectory chain, which has slack once the alpha
+                // chain is the pipeline's critical one
+                o[2 * (size_t)a.n] = sqrt_pos(N2);
+                o[4 * (size_t)a.n] = exp_fast<true>(p.lnTe);
             } else {
                 // |N|^2 and ln Te: k_alpha_pts takes the square root and the
                 // exponential (the same functions ray_rhs applies), off the
@@ -992,8 +1001,9 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
 #ifndef TORJ_TRAJ_WAVES
 #define TORJ_TRAJ_WAVES TORJ_MIN_WAVES
 #endif
-#ifndef TORJ_ALPHA_WAVES
-#define TORJ_ALPHA_WAVES 4
+#ifndef TORJ_ALPHA_WAVES  // k_alpha_pts' waves per SIMD bound (6: <= 80 VGPRs; round 5 with the tiny-alpha
+// skip, alternating: 40.01 / 40.01 ms against 40.23 / 40.12 at 4, 96 VGPRs; 8 spills: 48.6 ms)
+#define TORJ_ALPHA_WAVES 6
 #endif
 #ifndef TORJ_ALPHA_UNROLL  // node pairs per iteration of the alpha kernel's node loop (ILP)
 #define TORJ_ALPHA_UNROLL 1
@@ -1319,7 +1329,7 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
         }
     }
 #endif
-    const double Nabs = sqrt_pos(N2), Te = exp_fast<true>(lnTe);
+    const double Nabs = TORJ_AIN_TRAJ_MATH ? N2 : sqrt_pos(N2), Te = TORJ_AIN_TRAJ_MATH ? lnTe : exp_fast<true>(lnTe);
     if constexpr (COUNT) {
         AlbajarWork work = {};
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
