@@ -65,7 +65,10 @@ int torj_device_count(int *n);
  * Albajar resonance-ellipse integral (process-global, like the reference's
  * module globals _int_absz/_int_weights, src/constants.jl:7-8).  1 <= n <= 64.
  * Absorption calls fail with the reference's ErrorException message
- * (src/absorption.jl:173-175) until this has been called. */
+ * (src/absorption.jl:173-175) until this has been called.  Also reads
+ * TORJ_TINY_ALPHA (m^-1, default 1e-20; 0 = off): fixed-step ray tracing skips
+ * a harmonic integral whose rigorous bound on its share of alpha is below it
+ * (tau moves by < 2 TORJ_TINY_ALPHA per metre of ray). */
 int torj_abs_al_init(int n);
 
 /* ---- Plasma (src/plasma.jl:2-58) ----------------------------------------- */

@@ -1,7 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-O=gpurun_out/t7; mkdir -p $O
-bash scripts/gpu_ab.sh t7/ab base dw4 aw5 base dw4 aw5 || exit 1
-timeout -k 10 900 python -u -m pytest tests -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; echo "pytest rc=$?"
-tail -30 $O/pytest.log | grep -E "passed|failed|FAILED|Error"
+O=gpurun_out/t8; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_split.py -q -m gpu -k "streamed_deposition" --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1; echo "pytest rc=$?"; tail -3 $O/pytest.log
+bash scripts/gpu_env_ab.sh t8/env 'base:' 'd5:TORJ_DEPO_STREAM=5' 'd5l1:TORJ_DEPO_STREAM=5 TORJ_DEPO_LAG=1' 'd5l3:TORJ_DEPO_STREAM=5 TORJ_DEPO_LAG=3' 'base2:' 'd5b:TORJ_DEPO_STREAM=5' 'd5l1b:TORJ_DEPO_STREAM=5 TORJ_DEPO_LAG=1' 'd5l3b:TORJ_DEPO_STREAM=5 TORJ_DEPO_LAG=3' || exit 1

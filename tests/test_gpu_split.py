@@ -443,7 +443,7 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     out = {}
     old = os.environ.get("TORJ_DEPO_STREAM")
     try:
-        for mode in ("0", "1", "2", "3", "4"):
+        for mode in ("0", "1", "2", "3", "4", "5"):
             os.environ["TORJ_DEPO_STREAM"] = mode
             out[mode] = _run(T, hplasma, 3, 90, xp, Np, om, 1, **kw)
     finally:
@@ -462,8 +462,9 @@ def test_streamed_deposition_matches_one_pass(gpu, T, hplasma):
     # the windows on a stream of their own (TORJ_DEPO_STREAM=2, overlapping the
     # next block's scan): the same windows, so the same bits as on the scan's stream
     # and the split form (=3: a window's elimination and walk as two launches;
-    # =4: those two launches on a stream of their own)
-    for m in ("2", "3", "4"):
+    # =4: those two launches on a stream of their own; =5: on the trajectory
+    # kernel's stream, two blocks behind their scans)
+    for m in ("2", "3", "4", "5"):
         c = out[m]
         for f in ("state", "status", "steps", "P_dep", "dP_shell"):
             assert np.array_equal(getattr(b, f), getattr(c, f)), (m, f)

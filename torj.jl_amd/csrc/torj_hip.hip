@@ -3072,6 +3072,13 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     hipStream_t sT = serial ? s : p->streamT, s2 = serial ? s : p->stream2;
     hipStream_t s3 = serial ? s : (scan_own ? p->streamS : p->stream2);
     const bool depo_own = dstream && (dstream_env == 2 || dstream_env == 4) && !serial;
+    // =5: the windows' two launches on the trajectory kernel's stream, each
+    // window `lag` blocks behind its scan (TORJ_DEPO_LAG, default 2, < kRing):
+    // the walk's waves then alternate with the trajectory's instead of
+    // holding registers beside both it and the alpha kernel
+    const bool depo_traj = dstream && dstream_env == 5 && !serial;
+    const char *lag_e = getenv("TORJ_DEPO_LAG");
+    const int depo_lag = std::min(torj_plasma_s::kRing - 1, std::max(1, lag_e ? atoi(lag_e) : 2));
     if (depo_own && !p->streamD) {  // created on first use only: one more queue otherwise
         int lo = 0, hi = 0;
         HIPCK(hipDeviceGetStreamPriorityRange(&lo, &hi));
@@ -3144,6 +3151,13 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
         if (b >= R) HIPCK(hipStreamWaitEvent(sT, p->ev_S[r], 0));
+        if (depo_traj && b >= depo_lag) {  // block b - lag's window, behind its scan
+            const int bw = b - depo_lag;
+            HIPCK(hipStreamWaitEvent(sT, p->ev_S[bw % R], 0));
+            const int cap = (int)(first ? (bw == 0 ? first : first + (long)bw * kb) : std::min<long>((long)(bw + 1) * kb, n_steps));
+            hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sT, *fa, ds, sp.sinfo, cap);
+            hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sT, *fa, ds, sp.sinfo, cap);
+        }
         if (cell_traj)
             TORJ_SPLIT_DISPATCH(k_traj_cell, dim3(G), dim3(64), 0, sT, a, sp);
         else if (tile_traj)
@@ -3188,7 +3202,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         // (measured on the headline beam: after every block on the scan's stream
         // 3.62-3.63e9 ray-steps/s; every 2nd / 4th block 3.45-3.64 / 3.58-3.59e9;
         // behind the alpha or the trajectory kernel's stream 3.03 / 2.98e9)
-        if (dstream && b + 1 < n_blocks) {
+        if (dstream && !depo_traj && b + 1 < n_blocks) {
             if (depo_own) HIPCK(hipStreamWaitEvent(sD, p->ev_S[r], 0));
             if (dstream_env == 3 || dstream_env == 4) {  // elimination and walk as two launches
                 hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sD, *fa, ds, sp.sinfo, sp.k0 + sp.kb);
@@ -3200,14 +3214,22 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             }
         }
     }
+    if (depo_traj) {  // the last blocks' windows (every block's but the last, as above)
+        for (int bw = std::max(0, n_blocks - depo_lag); bw + 1 < n_blocks; bw++) {
+            HIPCK(hipStreamWaitEvent(sT, p->ev_S[bw % R], 0));
+            const int cap = (int)(first ? (bw == 0 ? first : first + (long)bw * kb) : std::min<long>((long)(bw + 1) * kb, n_steps));
+            hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sT, *fa, ds, sp.sinfo, cap);
+            hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sT, *fa, ds, sp.sinfo, cap);
+        }
+    }
     TORJ_SPLIT_DISPATCH(k_split_final, dim3(G), dim3(64), 0, s3, a, sp);
 #undef TORJ_SPLIT_DISPATCH
     if (!serial) {  // join: the final kernel followed every scan, each scan its alpha kernel
                     // and each alpha kernel its trajectory
         HIPCK(hipEventRecord(p->ev_J, s3));
         HIPCK(hipStreamWaitEvent(s, p->ev_J, 0));
-        if (depo_own) {
-            HIPCK(hipEventRecord(p->ev_D, sD));
+        if (depo_own || depo_traj) {
+            HIPCK(hipEventRecord(p->ev_D, depo_traj ? sT : sD));
             HIPCK(hipStreamWaitEvent(s, p->ev_D, 0));
         }
     }
