@@ -37,6 +37,28 @@ def test_abi_version_and_errors(T):
         T.abs_Al_init(0)
 
 
+def test_tiny_alpha_threshold_checked(T):
+    """TORJ_TINY_ALPHA (the bounded tiny-alpha skip) is read at
+    abs_Al_init: 0 and values below 1e-12 m^-1 are accepted, others refused with
+    the library's error (the skip's bound is only argued for thresholds far below
+    the parity bar's absolute floor)."""
+    old = os.environ.get("TORJ_TINY_ALPHA")
+    try:
+        for ok in ("0", "1e-20", "1e-15"):
+            os.environ["TORJ_TINY_ALPHA"] = ok
+            T.abs_Al_init(24)
+        for bad in ("1e-3", "-1e-20", "nan"):
+            os.environ["TORJ_TINY_ALPHA"] = bad
+            with pytest.raises(T.TorjError, match="TORJ_TINY_ALPHA"):
+                T.abs_Al_init(24)
+    finally:
+        if old is None:
+            os.environ.pop("TORJ_TINY_ALPHA", None)
+        else:
+            os.environ["TORJ_TINY_ALPHA"] = old
+        T.abs_Al_init(24)
+
+
 def test_plasma_coefficients_match_oracle(hplasma, oplasma):
     oc = oplasma.field_coefs()
     for k in ("psi", "lnne", "lnTe", "Br", "Bz", "Bphi"):
