@@ -382,8 +382,9 @@ def main():
                 "reference_algorithm_equivalent_TFLOPs":
                     F.algorithmic_flops_reference(cnt, n_gl=24) / kern_s / 1e12,
                 "note": "the reference algorithm's op count over the measured trace phase; the "
-                        "kernel skips part of that work bit-identically, so this is not achieved "
-                        "throughput (roofline.frac is)",
+                        "kernel skips part of that work (bit-identically, or below tiny_alpha = "
+                        "1e-20 m^-1 of absorption with tau moved by < 2e-20 per metre), so this is "
+                        "not achieved throughput (roofline.frac is)",
             } if args.absorption == "albajar" else None),
             "work_counters": (
                 {"ray_steps": int(cnt[0]), "rhs_evals": int(cnt[1]),
