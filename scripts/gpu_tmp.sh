@@ -1,4 +1,4 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-ROUND=r05 bash scripts/gpu_round.sh B || exit 1
+bash scripts/gpu_env_ab.sh t10/env 'base:' 'as2:TORJ_ALPHA_STREAMS=2' 'base2:' 'as2b:TORJ_ALPHA_STREAMS=2' || exit 1
