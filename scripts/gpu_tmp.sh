@@ -1,4 +1,6 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-bash scripts/gpu_ab.sh t12/ab base tp3 tp3ap1 base tp3 tp3ap1 || exit 1
+rm -rf gpurun_out/round gpurun_out/prof_c3 gpurun_out/prof_c5
+ROUND=r05 bash scripts/gpu_round.sh A || exit 1
+ROUND=r05 bash scripts/gpu_round.sh B || exit 1
