@@ -1115,8 +1115,12 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
+    // the remainder pairs (none when U = 1: the compiler still materialised the
+    // pair's constants for this loop's preheader, ~67 SALU per node loop)
+    if constexpr (U > 1) {
 #pragma unroll 1
-    for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, nd[i].t, nd[i].s2, nd[i].wm, nd[i].t2, false);
+        for (; i < half; i++) acc[0] += pair_term<M, LV>(c, sc, nd[i].t, nd[i].s2, nd[i].wm, nd[i].t2, false);
+    }
     if (n & 1) acc[0] += pair_term<M, LV>(c, sc, nd[half].t, nd[half].s2, nd[half].wm, nd[half].t2, true);
     double s = acc[0];
 #pragma unroll
