@@ -37,6 +37,10 @@ HBM_PEAK_BPS = 8.0e12  # MI355X HBM3E (MI355X_MICROARCH.md)
 # least the GPU Weideman Faddeeva's own relative error (2.5e-14), so the flag
 # covers the implementation's error as well as the reference's rounding
 WARM_FLAG_ETA = 2.0 ** -45
+# parity's unfloored tau statistic covers the sampled rays with tau_cpu at least this
+TAU_RESOLVABLE = 1e-12
+# the library's default tiny-alpha threshold (torj_hip.hip kTinyAlpha; env TORJ_TINY_ALPHA)
+TINY_ALPHA_DEFAULT = 1e-20
 ABSORPTION = {"none": 0, "albajar": 1, "warm_wr": 2, "warm_fr": 3}
 # the split RK4 pipeline's kernels (trajectory, alpha points, optical-depth scan, final)
 SPLIT_KERNELS = "k_traj|k_alpha_pts|k_tau_scan|k_split_final"
@@ -87,6 +91,8 @@ def parse():
                          "(profiling passes)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0,
                     help="target CPU time of the bounded cpu_baseline sample")
+    ap.add_argument("--no-exact", action="store_true",
+                    help="skip the exact leg (the same timed loop with TORJ_TINY_ALPHA=0)")
     ap.add_argument("--no-beam-host", action="store_true",
                     help="skip the C4-scale torj_trace_beam host-pointer call (N = 1)")
     ap.add_argument("--parity-rays", type=int, default=128,
@@ -252,14 +258,20 @@ def main():
         torch.cuda.synchronize(dev)
         reduce_ms = (time.perf_counter() - t_r) / 20 * 1e3
         mine = torch.tensor([kern_ms, post_ms, hot_ms, elapsed / args.steps * 1e3, float(n),
-                             float(ray_steps_local), reduce_ms], dtype=torch.float64, device=dev)
+                             float(ray_steps_local), reduce_ms, float(torch.cuda.current_device()),
+                             float(dist.get_rank()), float(dist.get_world_size())],
+                            dtype=torch.float64, device=dev)
         allr = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(allr, mine)
         rows = [a.cpu().numpy() for a in allr]
         per_rank = {"trace_ms": [float(r[0]) for r in rows], "deposition_ms": [float(r[1]) for r in rows],
                     "call_ms": [float(r[2]) for r in rows], "step_ms": [float(r[3]) for r in rows],
                     "rays": [int(r[4]) for r in rows], "ray_steps": [int(r[5]) for r in rows],
-                    "rccl_allreduce_ms": [float(r[6]) for r in rows]}
+                    "rccl_allreduce_ms": [float(r[6]) for r in rows],
+                    # who took part: each rank's HIP device (torch.cuda.current_device) and its
+                    # rank / size in the process group the all_reduce ran over
+                    "device": [int(r[7]) for r in rows], "pg_rank": [int(r[8]) for r in rows],
+                    "pg_size": [int(r[9]) for r in rows], "backend": dist.get_backend()}
         dist.all_reduce(tot_steps)
         dist.all_reduce(el, op=dist.ReduceOp.MAX)
         dist.all_reduce(km, op=dist.ReduceOp.MAX)
@@ -270,7 +282,10 @@ def main():
 
     if rank == 0:
         status = d_status.cpu().numpy()
-        flop = (F.algorithmic_flops(cnt, n_gl=24) if args.absorption in ("albajar", "none")
+        # the headline launches' outputs (the parity sample's GPU side), before any
+        # later leg reuses the buffers
+        gpu_out = (d_state.cpu().numpy().T.copy(), status.copy(), d_steps.cpu().numpy())
+        flop =(F.algorithmic_flops(cnt, n_gl=24) if args.absorption in ("albajar", "none")
                 else F.algorithmic_flops_warm(cnt) if args.absorption == "warm_wr" else None)
         n_simd = 4 * torch.cuda.get_device_properties(dev).multi_processor_count
         sched = adaptive or (os.environ.get("TORJ_SCHED", "1") != "0" and (n + 63) // 64 > n_simd)
@@ -330,6 +345,9 @@ def main():
                 "n_psi": args.n_psi,
                 "traj_stride": args.traj_stride,
                 "absorption": args.absorption,
+                # harmonics whose rigorous share of alpha is below this are not
+                # integrated (m^-1; 0 = every integral, the reference's work)
+                "tiny_alpha": tiny_alpha() if args.absorption == "albajar" else None,
                 "build_id": L.torj_build_id().decode(),
                 "torj_env": torj_env(),
                 "parallelism": (f"ray-shard x{world} on ONE device (TORJ_BENCH_SAME_DEVICE rehearsal, "
@@ -420,14 +438,21 @@ def main():
                 out["host_api_beam_c4"] = host_beam_c4(T, plasma, cfg, args, omega, n_save)
                 progress("C4-scale torj_trace_beam call done")
             out["ray_entry"] = entry_timing(T, plasma, pos, dirs, omega, args.mode, t_entry)
+        exact_out = None
+        if (world == 1 and args.absorption == "albajar" and not adaptive and not args.no_exact
+                and tiny_alpha() > 0.0):
+            out["exact"], exact_out = exact_leg(T, L, plasma, launch, dev, args, value, kern_ms, post_ms,
+                                                d_state, d_status, d_steps, gpu_out)
+            progress("exact (TORJ_TINY_ALPHA=0) leg done")
         if world == 1 and not args.no_cpu_baseline:
-            gpu_out = (d_state.cpu().numpy().T, status, d_steps.cpu().numpy())
-            out["cpu_baseline"], parity = cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out)
+            out["cpu_baseline"], parity = cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out,
+                                                       exact_out)
             if parity is not None:
+                if exact_out is not None:
+                    out["exact"]["parity"] = parity.pop("exact")
                 out["parity"] = parity
         elif world > 1 and args.parity_rays > 0 and args.integrator == "rk4":
             # rank 0's shard against the oracle (bounded sample, untimed)
-            gpu_out = (d_state.cpu().numpy().T, status, d_steps.cpu().numpy())
             out["parity"] = parity_sample(eq, xp, Np, w, omega, args, grid, gpu_out, args.parity_rays)
             out["parity"]["shard"] = "rank 0"
         check_line(out)
@@ -460,7 +485,7 @@ def main_library(args):
     import torj_hip as T
     from torj_hip import flops as F
     from torj_hip import synthetic as S
-    from torj_hip.parallel import group_shard, trace_beam_device
+    from torj_hip.parallel import beam_comm_info, group_shard, trace_beam_device
 
     N = args.gpus
     eq = S.circular_tokamak()
@@ -623,7 +648,10 @@ def main_library(args):
         "multi_gpu": multi_gpu_block(
             {"trace_ms": trace_ms, "deposition_ms": dep_ms, "call_ms": [ms_per_step] * N,
              "step_ms": [ms_per_step] * N, "rays": [sh["n"] for sh in shards],
-             "ray_steps": [int(c[0]) for c in cnt], "rccl_allreduce_ms": [rccl_ms] * N},
+             "ray_steps": [int(c[0]) for c in cnt], "rccl_allreduce_ms": [rccl_ms] * N,
+             # torj_beam_comm_info: each replica's HIP device and its RCCL communicator's
+             # rank count / rank (ncclCommCount / ncclCommUserRank; 0 / -1: no communicator)
+             **beam_comm_info(plasma, N)},
             path="one process: torj_trace_beam_device, a host thread + stream per device, the "
                  "library's RCCL all-reduce (ncclCommInitAll)"),
     }
@@ -644,7 +672,10 @@ LINE_KEYS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_ste
              "scaling", "vs_baseline", "dtype", "data", "config", "roofline")
 MULTI_GPU_KEYS = ("path", "trace_ms_per_device", "deposition_ms_per_device", "call_ms_per_device",
                   "rays_per_device", "ray_steps_per_device", "trace_ms_max", "trace_ms_min",
-                  "imbalance", "rccl_allreduce_ms")
+                  "imbalance", "rccl_allreduce_ms", "device")
+# and who took part in the reduce, per path: the library path's RCCL communicator
+# (torj_beam_comm_info), torchrun's process group
+MULTI_GPU_COMM_KEYS = {"library": ("rccl_nranks", "rccl_rank"), "torchrun": ("pg_rank", "pg_size", "backend")}
 
 
 def multi_gpu_block(per, path):
@@ -653,7 +684,9 @@ def multi_gpu_block(per, path):
     ray-steps, the spread of the trace phase (max / min - 1) and the RCCL
     all-reduce of make_beam's reduce (src/solve.jl:233-240)."""
     tr = [float(v) for v in per["trace_ms"]]
-    return {"path": path,
+    extra = {k: per[k] for k in ("device", "pg_rank", "pg_size", "backend", "rccl_nranks", "rccl_rank")
+             if k in per}
+    return {"path": path, **extra,
             "trace_ms_per_device": tr,
             "deposition_ms_per_device": [float(v) for v in per["deposition_ms"]],
             "call_ms_per_device": [float(v) for v in per["call_ms"]],
@@ -673,8 +706,11 @@ def check_line(out):
         mg = out.get("multi_gpu")
         if mg is None or any(k not in mg for k in MULTI_GPU_KEYS):
             raise KeyError("an N >= 2 line needs the multi_gpu block with " + ", ".join(MULTI_GPU_KEYS))
-        if len(mg["trace_ms_per_device"]) != out["n_gpus"]:
-            raise ValueError("multi_gpu: one trace_ms entry per device")
+        if len(mg["trace_ms_per_device"]) != out["n_gpus"] or len(mg["device"]) != out["n_gpus"]:
+            raise ValueError("multi_gpu: one trace_ms and one device entry per device")
+        if not any(all(k in mg for k in ks) for ks in MULTI_GPU_COMM_KEYS.values()):
+            raise KeyError("multi_gpu: the reduce's participants (" + " or ".join(
+                ", ".join(ks) for ks in MULTI_GPU_COMM_KEYS.values()) + ")")
     return out
 
 
@@ -788,6 +824,66 @@ def entry_timing(T, plasma, pos, dirs, omega, mode, t_first):
             "host_threads": int(os.environ.get("OMP_NUM_THREADS", "0") or os.cpu_count())}
 
 
+def tiny_alpha():
+    """The tiny-alpha threshold the library reads at abs_Al_init (m^-1)."""
+    v = os.environ.get("TORJ_TINY_ALPHA")
+    return float(v) if v is not None else TINY_ALPHA_DEFAULT
+
+
+def exact_leg(T, L, plasma, launch, dev, args, value_main, trace_ms_main, post_ms_main, d_state,
+              d_status, d_steps, gpu_out_main):
+    """The headline's timed loop again with TORJ_TINY_ALPHA=0: every harmonic
+    integral with m >= m_0 evaluated, as the reference does (src/absorption.jl:
+    213-223), so what the default's bounded tiny-alpha skip buys
+    is visible beside it.  min(steps, 10) launches after one warm one, the host
+    clock with the device drained on both sides (the headline's timed region) and
+    the library's HIP events for the trace / deposition phases.  Returns the
+    leg's figures and its outputs (state, status, steps) for the parity sample."""
+    import ctypes
+
+    import torch
+
+    old = os.environ.get("TORJ_TINY_ALPHA")
+    os.environ["TORJ_TINY_ALPHA"] = "0"
+    try:
+        T.abs_Al_init(24)
+        launch()
+        torch.cuda.synchronize(dev)
+        k = max(1, min(args.steps, 10))
+        T._lib.check(L.torj_timing(plasma.handle, 1))
+        t0 = time.perf_counter()
+        for _ in range(k):
+            launch()
+        torch.cuda.synchronize(dev)
+        dt = (time.perf_counter() - t0) / k
+        n_calls, t_trace, t_post = ctypes.c_int(), ctypes.c_double(), ctypes.c_double()
+        T._lib.check(L.torj_timing_read(plasma.handle, ctypes.byref(n_calls), ctypes.byref(t_trace),
+                                        ctypes.byref(t_post)))
+        T._lib.check(L.torj_timing(plasma.handle, 0))
+        out = (d_state.cpu().numpy().T.copy(), d_status.cpu().numpy(), d_steps.cpu().numpy())
+    finally:
+        if old is None:
+            del os.environ["TORJ_TINY_ALPHA"]
+        else:
+            os.environ["TORJ_TINY_ALPHA"] = old
+        T.abs_Al_init(24)
+    ray_steps = float(out[2].astype(np.int64).sum())
+    trace_ms = t_trace.value / max(n_calls.value, 1)
+    s0, s1 = gpu_out_main[0][:, 6], out[0][:, 6]
+    return {"tiny_alpha": 0.0,
+            "value": ray_steps / dt, "unit": "ray-steps/s", "ms_per_step": dt * 1e3, "steps": k,
+            "trace_ms": trace_ms, "deposition_ms": t_post.value / max(n_calls.value, 1),
+            "headline_over_exact": value_main / (ray_steps / dt),
+            "trace_ms_saved_by_tiny_alpha": trace_ms - trace_ms_main,
+            "status_equal_headline": bool(np.array_equal(out[1], gpu_out_main[1])),
+            "steps_equal_headline": bool(np.array_equal(out[2], gpu_out_main[2])),
+            "xN_equal_headline": bool(np.array_equal(out[0][:, :6], gpu_out_main[0][:, :6])),
+            "max_abs_tau_diff_headline": float(np.abs(s1 - s0).max()),
+            "note": "the same launches with TORJ_TINY_ALPHA=0 (every harmonic integral evaluated); "
+                    "the headline skips a harmonic whose rigorous share of alpha is below "
+                    "config.tiny_alpha m^-1"}, out
+
+
 def torj_env():
     """The TORJ_* switches of this process (kernel variants, schedules): a
     profile is paired only with a run under the same switches."""
@@ -878,12 +974,19 @@ def _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads):
     # it the bar is 1e-16 absolute
     et = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-6)
     et_strict = np.abs(gs[:, 6] - os_[:, 6]) / np.maximum(np.abs(os_[:, 6]), 1e-300)
+    # unfloored relative tau over the rays whose tau a result can resolve
+    # (tau_cpu >= 1e-12): the tiny-alpha skip's share there is bounded by
+    # 2e-20 per metre / 1e-12
+    resolv = np.abs(os_[:, 6]) >= TAU_RESOLVABLE
     parity = {"rays": int(len(idx)), "vs": "oracle/torj_oracle.c (same RK4, same rays)",
               "status_equal": bool(np.array_equal(gst, r["status"])),
               "steps_equal": bool(np.array_equal(gk, r["steps"])),
               "max_rel_x": float(ex.max()), "max_rel_N": float(eN.max()),
               "max_rel_tau": float(et.max()), "tau_floor": 1e-6,
               "max_rel_tau_unfloored": float(et_strict.max()),
+              "tau_resolvable": TAU_RESOLVABLE,
+              "rays_tau_resolvable": int(resolv.sum()),
+              "max_rel_tau_resolvable": float(et_strict[resolv].max()) if resolv.any() else None,
               # below the floor the bar is absolute: the largest |tau_gpu - tau_cpu| there
               # (the tiny-alpha skip moves tau by < 2e-20 per metre of ray)
               "max_abs_tau_below_floor": float(np.where(np.abs(os_[:, 6]) < 1e-6,
@@ -958,13 +1061,15 @@ def parity_sample(eq, xp, Np, w, omega, args, grid, gpu_out, n_rays):
     return _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads)
 
 
-def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
+def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out, exact_out=None):
     """The CPU oracle (C restatement, OpenMP on every host core) on a bounded
     sample of the same rays, warm models included (oracle/torj_warm_oracle.c).
     Returns (cpu_baseline, parity): when the sample runs the full n_steps, parity
     compares its endpoints with the timed launches' GPU outputs for the same rays
     (status / steps exact, max relative error of x, N, tau; bar 1e-10, warm models
-    the tests' 1e-8 / 1e-9 on tau, tests/test_gpu_warm.py)."""
+    the tests' 1e-8 / 1e-9 on tau, tests/test_gpu_warm.py); with exact_out (the
+    TORJ_TINY_ALPHA=0 leg's outputs) parity["exact"] holds the same comparison
+    for that leg against the same oracle run."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     from torj_hip import synthetic as S
@@ -991,7 +1096,9 @@ def cpu_baseline(eq, xp, Np, w, omega, args, grid, gpu_out):
     parity = None
     if n_steps == args.n_steps and args.integrator == "rk4":
         parity = _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads)
-    what = ("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
+        if exact_out is not None:
+            parity["exact"] = _parity(OP, r, idx, xp, Np, omega, args, exact_out, threads)
+    what =("oracle/torj_oracle.c RK4 + oracle/torj_warm_oracle.c warm alpha, OpenMP" if warm
             else "oracle/torj_oracle.c OpenMP")
     return {"value": steps / dt, "unit": "ray-steps/s", "cores": threads, "kind": "port",
             "sample": f"{n_rays} rays (evenly spaced over the same fan) x {n_steps} RK4 steps, "

@@ -34,10 +34,10 @@
 extern "C" {
 #endif
 
-#define TORJ_ABI_VERSION 7  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
+#define TORJ_ABI_VERSION 8  /* 3: torj_trace_beam, sticky launch flags; 4: 8 work counters;
                                5: torj_trace_beam_device, torj_power_deposition_profile;
                                6: torj_beam_timing_read, torj_trace_beam's automatic shards;
-                               7: torj_build_id */
+                               7: torj_build_id; 8: torj_beam_comm_info */
 
 /* per-ray status codes (replace the reference's @assert / unhandled returns) */
 enum torj_status {
@@ -348,6 +348,16 @@ int torj_timing_read(torj_plasma_t p, int *calls, double *trace_ms, double *post
  * stream waits).  Clears what it reads. */
 int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace_ms, double *post_ms,
                           double *reduce_ms);
+
+/* Who took part in make_beam's reduce (src/solve.jl:233-240) of the last
+ * torj_trace_beam[_device] fan-out over n_gpus replicas (measurement support,
+ * no reference counterpart): per replica k, the HIP device it ran on
+ * (device[k]), and its RCCL communicator's rank count (ncclCommCount) and
+ * rank (ncclCommUserRank) in nranks[k] / rank[k] -- or 0 / -1 where no
+ * communicator exists (one replica without TORJ_BEAM_RCCL=1: nothing to
+ * reduce; the test-only same-device placement: partials summed on the host).  Arrays of n_gpus
+ * entries; n_gpus may not exceed the handle's replicas. */
+int torj_beam_comm_info(torj_plasma_t p, int n_gpus, int *device, int *nranks, int *rank);
 
 /* power_deposition_profile(plasma, s, x, dP_ds, psi_dP_dV) (src/plasma.jl:91-151)
  * on the GPU for n_rays rays at once: ray r has n_points[r] >= 4 points with

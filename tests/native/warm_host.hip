@@ -28,6 +28,14 @@ void wh_ssbi(double z, int n, int l, double *out) {
     for (int m = 0; m <= l + 2 - n; m++) out[m] = v[m];
 }
 
+// the product's complex square root (torj_warm.hpp csqrt_), n points
+void wh_csqrt(int n, const double *re, const double *im, double *out_re, double *out_im) {
+    for (int i = 0; i < n; i++) {
+        const torj::cplx r = torj::csqrt_(torj::cplx{re[i], im[i]});
+        out_re[i] = r.re;
+        out_im[i] = r.im;
+    }
+}
 int wh_larmornumber(double yg, double npl, double mu) { return torj::larmornumber(yg, npl, mu); }
 
 // the product's Julia round(Int64, x) (launch ring point counts, src/launch.jl:81)

@@ -63,8 +63,12 @@ def test_multi_gpu_line_schema():
     B = _bench_module()
     per = {"trace_ms": [50.0, 52.0], "deposition_ms": [1.0, 1.1], "call_ms": [55.0, 56.0],
            "step_ms": [56.0, 56.0], "rays": [100203, 100203], "ray_steps": [200406000, 200406000],
-           "rccl_allreduce_ms": [0.05, 0.06]}
+           "rccl_allreduce_ms": [0.05, 0.06], "device": [0, 1], "rccl_nranks": [2, 2],
+           "rccl_rank": [0, 1]}
     mg = B.multi_gpu_block(per, path="test")
+    # the reduce's participants pass through: each replica's device and its RCCL
+    # communicator's rank count / rank (torj_beam_comm_info)
+    assert mg["device"] == [0, 1] and mg["rccl_nranks"] == [2, 2] and mg["rccl_rank"] == [0, 1]
     assert set(B.MULTI_GPU_KEYS) <= set(mg)
     assert mg["trace_ms_max"] == 52.0 and mg["trace_ms_min"] == 50.0
     assert abs(mg["imbalance"] - 0.04) < 1e-12 and mg["rccl_allreduce_ms"] == 0.06
@@ -74,6 +78,16 @@ def test_multi_gpu_line_schema():
         B.check_line(_line(2))
     with pytest.raises(ValueError):
         B.check_line(_line(3, multi_gpu=mg))
+    # torchrun's form: the process group's ranks instead of a library communicator
+    tr = B.multi_gpu_block(dict(per, pg_rank=[0, 1], pg_size=[2, 2], backend="nccl"), path="t")
+    for k in ("rccl_nranks", "rccl_rank"):
+        tr.pop(k)
+    B.check_line(_line(2, multi_gpu=tr))
+    anon = dict(mg)
+    for k in ("rccl_nranks", "rccl_rank"):
+        anon.pop(k)
+    with pytest.raises(KeyError):  # no participants named
+        B.check_line(_line(2, multi_gpu=anon))
     bad = _line(2, multi_gpu=mg)
     del bad["roofline"]
     with pytest.raises(KeyError):

@@ -28,7 +28,7 @@ def test_library_exports_every_declared_symbol(T):
 
 
 def test_abi_version_and_errors(T):
-    assert T.lib().torj_abi_version() == T._lib.ABI_VERSION == 7
+    assert T.lib().torj_abi_version() == T._lib.ABI_VERSION == 8
     bid = T.lib().torj_build_id().decode()
     assert re.fullmatch(r"[0-9a-f]{16}", bid), bid
     with pytest.raises(ValueError, match="N_rings"):

@@ -208,6 +208,12 @@ def test_trace_beam_device_shards_threaded(gpu, T, hplasma):
         assert list(calls) == [1, 1, 1] and all(t > 0 for t in t_tr) and all(t > 0 for t in t_po)
         assert t_red.value >= 0.0
         assert L.torj_beam_timing_read(hplasma.handle, 9, calls, t_tr, t_po, None) != 0  # 3 replicas
+        # torj_beam_comm_info: three replicas on device 0, no communicator (host sum)
+        from torj_hip.parallel import beam_comm_info
+        ci = beam_comm_info(hplasma, 3)
+        assert ci == {"device": [0, 0, 0], "rccl_nranks": [0, 0, 0], "rccl_rank": [-1, -1, -1]}, ci
+        assert L.torj_beam_comm_info(hplasma.handle, 9, (C.c_int * 9)(), (C.c_int * 9)(),
+                                     (C.c_int * 9)()) != 0
         c1 = torch.zeros(8, dtype=torch.int64, device=dev)
         one = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0, [slice(0, n)], dev)
         one[0]["counters"] = c1
@@ -227,9 +233,28 @@ def test_trace_beam_device_shards_threaded(gpu, T, hplasma):
     assert np.array_equal(one[0]["dP_shell"].cpu().numpy(), a.dP_shell)
 
 
+def test_trace_beam_one_replica_rccl_comm_info(gpu, T, hplasma):
+    """One replica with the RCCL reduce forced (TORJ_BEAM_RCCL=1): a real
+    one-rank communicator on device 0, which torj_beam_comm_info reports (rank
+    count 1, rank 0); dP_shell is unchanged by the one-rank all-reduce."""
+    from torj_hip.parallel import beam_comm_info
+
+    pos, xp, Np, s0, w, om = _beam(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=200, psi_grid=np.linspace(0, 1, 100), weights=w, x_launch=pos, s0=s0)
+    a = T.trace(hplasma, xp, Np, om, 1, n_gpus=1, **kw)
+    with _env(TORJ_BEAM_RCCL="1"):
+        b = T.trace(hplasma, xp, Np, om, 1, n_gpus=1, **kw)
+    assert beam_comm_info(hplasma, 1) == {"device": [0], "rccl_nranks": [1], "rccl_rank": [0]}
+    assert np.array_equal(a.dP_shell, b.dP_shell)
+
+
 def test_trace_beam_two_devices(gpu, T, hplasma):
-    """n_gpus = 2 on two real devices (skipped on a one-GPU box): RCCL
-    all-reduce over xGMI, per-ray bit-identical to the unsplit launch."""
+    """n_gpus = 2 on two real devices (skipped only on a one-GPU box; with two
+    or more devices visible it runs and must pass): RCCL all-reduce over xGMI,
+    per-ray bit-identical to the unsplit launch, and the communicator spans two
+    ranks on two distinct devices (torj_beam_comm_info)."""
+    from torj_hip.parallel import beam_comm_info
+
     if gpu < 2:
         pytest.skip(f"needs two HIP devices, {gpu} visible")
     pos, xp, Np, s0, w, om = _beam(T, hplasma)
@@ -239,9 +264,12 @@ def test_trace_beam_two_devices(gpu, T, hplasma):
         hplasma.set_sched(0)
         a = T.trace(hplasma, xp, Np, om, 1, **kw)
         b = T.trace(hplasma, xp, Np, om, 1, n_gpus=2, **kw)
+        ci = beam_comm_info(hplasma, 2)
     finally:
         hplasma.set_sched(-1)
     _same(a, b)
+    assert ci["rccl_nranks"] == [2, 2] and sorted(ci["rccl_rank"]) == [0, 1], ci
+    assert len(set(ci["device"])) == 2, ci
 
 
 def test_c4_million_ray_beam_sharded_rccl_batched(gpu, T, hplasma, oplasma):

@@ -79,6 +79,67 @@ def test_c3_fan_reference_deposition_vs_fitpack(c3, oplasma):
         assert abs(g.P_dep[i] - P) <= 1e-11 * P + 2e-20 * DS * o["steps"][k], (i, g.P_dep[i], P)
 
 
+@pytest.fixture(scope="module")
+def c3_exact(c3, T, hplasma):
+    """The headline beam again with TORJ_TINY_ALPHA=0 (read at abs_Al_init): every
+    harmonic integral with m >= m_0 evaluated, the reference's work."""
+    import os
+
+    old = os.environ.get("TORJ_TINY_ALPHA")
+    os.environ["TORJ_TINY_ALPHA"] = "0"
+    try:
+        T.abs_Al_init(24)
+        hplasma.set_sched(-1)
+        return T.trace(hplasma, c3["xp"], c3["Np"], c3["om"], 1, **c3["kw"])
+    finally:
+        if old is None:
+            del os.environ["TORJ_TINY_ALPHA"]
+        else:
+            os.environ["TORJ_TINY_ALPHA"] = old
+        T.abs_Al_init(24)
+
+
+def test_c3_fan_exact_leg_vs_fitpack(c3, c3_exact, oplasma):
+    """The exact leg keeps the pre-round-5 bars: P_dep of the same 24 rays within
+    1e-11 of FITPACK's power_deposition_profile, purely relative (no tiny-alpha
+    term); statuses, steps and x, N bit-identical to the default leg (the skip
+    touches alpha only); tau of the default leg within its bound of the exact one."""
+    import deposition_ref as D
+
+    g, ge = c3["g"], c3_exact
+    for f in ("status", "steps"):
+        assert np.array_equal(getattr(g, f), getattr(ge, f)), f
+    assert np.array_equal(g.state[:, :6], ge.state[:, :6])
+    # the default leg's tau moves by < 2 tiny_alpha per metre of ray (1e-20 m^-1)
+    assert np.abs(g.state[:, 6] - ge.state[:, 6]).max() <= 2e-20 * DS * N_STEPS * 1.01
+    idx = np.linspace(0, len(c3["w"]) - 1, 24).astype(int)
+    o = oplasma.trace(c3["xp"][idx], c3["Np"][idx], c3["om"], 1, DS, N_STEPS, samples=True,
+                      s0=c3["s0"][idx])
+    assert np.array_equal(o["steps"], ge.steps[idx])
+    for k, i in enumerate(idx):
+        sv, psi, dpds = D.ray_vectors(c3["pos"][i], c3["s0"][i], DS, o["steps"][k],
+                                      o["samples"][k], oplasma.evaluate("psi", c3["pos"][i]))
+        _, P = D.power_deposition_profile(sv, psi, dpds, c3["grid"], oplasma.volume)
+        assert abs(ge.P_dep[i] - P) <= 1e-11 * P, (i, ge.P_dep[i], P)
+
+
+def test_c3_fan_exact_leg_tau_unfloored(c3, c3_exact, oplasma):
+    """Every 25th ray: the exact leg's tau against the oracle with no floor at all
+    (relative to tau_cpu wherever tau_cpu > 0); the default leg's unfloored tau on
+    the rays with tau_cpu >= 1e-10 (where its rigorous bound, 2e-20 per metre /
+    1e-10 = 4e-11 over the 0.2 m path, is inside the 1e-10 bar)."""
+    idx = np.arange(0, len(c3["w"]), 25)
+    o = oplasma.trace(c3["xp"][idx], c3["Np"][idx], c3["om"], 1, DS, N_STEPS,
+                      psi_grid=c3["grid"], weights=c3["w"][idx])
+    tc = o["state"][:, 6]
+    pos = tc > 0
+    e_exact = np.abs(c3_exact.state[idx, 6] - tc)[pos] / tc[pos]
+    assert e_exact.max() <= 1e-10, e_exact.max()
+    res = tc >= 1e-10
+    e_def = np.abs(c3["g"].state[idx, 6] - tc)[res] / tc[res]
+    assert e_def.max() <= 1e-10, e_def.max()
+
+
 def _close(a, b, tol, tau_floor=1e-13):
     """Per-ray outputs equal to rounding: the split path's kernels are compiled
     separately from the fused one, so fma contraction may differ (~1e-15 on x, N;

@@ -252,3 +252,23 @@ def test_albajar_negligible_harmonic_skip_is_bit_identical(H):
     H.wh_set_negl_skip(1)
     assert skipped > 0.2 * len(rows)
     assert early > 0.1 * len(rows)
+
+
+@pytest.mark.parametrize("scale", [1e-170, 1e-160, 1e-3, 1.0, 1e3, 1e160, 1e170, 1e300])
+def test_csqrt_extreme_magnitudes(H, scale):
+    """warmdisp's complex square root (csqrt_) over |z| from 1e-170 to 1e300:
+    where |z|^2 underflows or overflows it falls back to hypot, so near mode
+    coupling (rr -> 0) the root stays small and finite, and matches numpy's
+    principal branch to ~2 ulp everywhere, including re == 0 with a tiny im."""
+    rng = np.random.default_rng(11)
+    n = 2000
+    ang = rng.uniform(-np.pi, np.pi, n)
+    re, im = scale * np.cos(ang), scale * np.sin(ang)
+    re[:4], im[:4] = 0.0, [scale, -scale, 0.5 * scale, 3.0 * scale]  # the pure-imaginary edge
+    im[4:8], re[4:8] = 0.0, [scale, -scale, 2.0 * scale, -0.25 * scale]
+    ore, oim = np.zeros(n), np.zeros(n)
+    H.wh_csqrt(n, _d(re), _d(im), _d(ore), _d(oim))
+    got = ore + 1j * oim
+    ref = np.sqrt(re + 1j * im)
+    assert np.isfinite(got).all()
+    assert (np.abs(got - ref) / np.abs(ref)).max() <= 4e-16, scale

@@ -18,6 +18,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdarg>
@@ -1272,8 +1273,15 @@ template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_tile(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, kTrajTile>(a, sp);
 }
+// measurement knob: a VGPR budget for the cell kernel between the 2- and 3-wave
+// bounds (176: two trajectory waves and two 80-VGPR alpha waves share a SIMD)
+#ifdef TORJ_TRAJ_CELL_VGPR
+#define TORJ_TRAJ_CELL_ATTR __attribute__((amdgpu_num_vgpr(TORJ_TRAJ_CELL_VGPR)))
+#else
+#define TORJ_TRAJ_CELL_ATTR
+#endif
 template <int DEPO, bool TRAJ>
-__global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_cell(TraceArgs a, SplitArgs sp) {
+__global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) TORJ_TRAJ_CELL_ATTR k_traj_cell(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, kTrajCell>(a, sp);
 }
 
@@ -3118,8 +3126,16 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const int tile_max = lds_env == 3 ? kTileCells : kTileNodes;  // cells / nodes
     sp.tile_cap = std::min(tile_max, cap_e ? atoi(cap_e) : tile_max);
     sp.tile_margin = mar_e ? atof(mar_e) : 1.001;
+    // test hook only (tests/test_gpu_split.py): the scan reads alpha as NaN at
+    // this step for every third ray -- a stray setting corrupts results, so say so
     const char *nan_e = getenv("TORJ_TEST_NAN_ALPHA_STEP");
     sp.nan_step = nan_e ? atoi(nan_e) : -1;
+    if (sp.nan_step >= 0) {
+        static std::atomic<bool> warned{false};
+        if (!warned.exchange(true))
+            fprintf(stderr, "libtorj_hip: TORJ_TEST_NAN_ALPHA_STEP=%d is set -- a TEST HOOK: alpha is "
+                            "read as NaN at that step for every third ray\n", sp.nan_step);
+    }
     const char *dl_e = getenv("TORJ_WARM_DEFER_LRM");
     sp.defer_lrm = dl_e ? std::min(3, std::max(0, atoi(dl_e))) : 3;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
@@ -3532,19 +3548,6 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
         else                                \
             TORJ_DISPATCH_D(L, 0);          \
     } while (0)
-    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
-    if (p->timing) {
-        if (p->ev_used + 3 > p->ev_pool.size()) {
-            for (int q = 0; q < 3; q++) {
-                hipEvent_t e;
-                HIPCK(hipEventCreate(&e));
-                p->ev_pool.push_back(e);
-            }
-        }
-        for (int q = 0; q < 3; q++) ev[q] = p->ev_pool[p->ev_used + q];
-        p->ev_used += 3;
-        HIPCK(hipEventRecord(ev[0], s));
-    }
     static const int split_env = [] {
         const char *e = getenv("TORJ_SPLIT");
         return e ? atoi(e) : 1;
@@ -3570,7 +3573,23 @@ static int trace_device_one(torj_plasma_t p, const torj_trace_cfg *cfg, int n, c
     const bool use_split = !adaptive && cfg->absorption >= 1 && cfg->n_steps > 0 &&
                            cfg->n_steps < kSplitMaxSteps &&
                            (p->sched_mode == 3 || (p->sched_mode < 0 && (albajar_split || warm_split)));
+    // the fused / queue paths clear the deposition workspace before the trace
+    // phase's first event (outside trace_ms, as before round 5); the split path
+    // clears it on its scan stream, overlapped with the first trajectory block
     if (fit && !use_split && fit_zero(fa, s)) return -1;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    if (p->timing) {
+        if (p->ev_used + 3 > p->ev_pool.size()) {
+            for (int q = 0; q < 3; q++) {
+                hipEvent_t e;
+                HIPCK(hipEventCreate(&e));
+                p->ev_pool.push_back(e);
+            }
+        }
+        for (int q = 0; q < 3; q++) ev[q] = p->ev_pool[p->ev_used + q];
+        p->ev_used += 3;
+        HIPCK(hipEventRecord(ev[0], s));
+    }
     if (use_split) {
         if (split_trace(p, a, DM, tr, cs, s, fit ? &fa : nullptr, &dstr)) return -1;
     } else if (use_sched && cfg->n_steps > 0) {
@@ -3790,11 +3809,13 @@ int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace
                           double *reduce_ms) {
     if (!p) return fail("bad plasma handle");
     if (n_gpus < 1) return fail("n_gpus must be >= 1");
-    if (n_gpus > std::max<int>(1, (int)p->replicas.size()))
-        return fail("n_gpus = %d, but the handle has %d replica(s)", n_gpus, std::max<int>(1, (int)p->replicas.size()));
     int dev0 = 0;
     HIPCK(hipGetDevice(&dev0));
-    std::lock_guard<std::mutex> lk(p->mu);  // the replica list (torj_timing takes it too)
+    // the replica list (torj_timing and beam_replicas take it too): held from the
+    // range check on, so a concurrent fan-out cannot change it in between
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (n_gpus > std::max<int>(1, (int)p->replicas.size()))
+        return fail("n_gpus = %d, but the handle has %d replica(s)", n_gpus, std::max<int>(1, (int)p->replicas.size()));
     int rc = 0;
     for (int k = 0; k < n_gpus && rc == 0; k++) {
         torj_plasma_s *q = k == 0 ? p : p->replicas[k];
@@ -3809,6 +3830,29 @@ int torj_beam_timing_read(torj_plasma_t p, int n_gpus, int *calls, double *trace
     if (reduce_ms) *reduce_ms = p->reduce_ms;
     p->reduce_ms = 0.0;
     p->reduce_calls = 0;
+    return 0;
+}
+
+int torj_beam_comm_info(torj_plasma_t p, int n_gpus, int *device, int *nranks, int *rank) {
+    if (!p) return fail("bad plasma handle");
+    if (n_gpus < 1) return fail("n_gpus must be >= 1");
+    if (!device || !nranks || !rank) return fail("device, nranks and rank must be arrays of n_gpus");
+    std::lock_guard<std::mutex> lk(p->mu);
+    if (n_gpus > std::max<int>(1, (int)p->replicas.size()))
+        return fail("n_gpus = %d, but the handle has %d replica(s)", n_gpus, std::max<int>(1, (int)p->replicas.size()));
+    // the communicator of the last RCCL reduce (beam_reduce_run keeps one per
+    // replica of that fan-out; rebuilt when the replica count changes)
+    const bool comm = (int)p->comms.size() == n_gpus;
+    for (int k = 0; k < n_gpus; k++) {
+        device[k] = (k == 0 ? p : p->replicas[k])->device;
+        nranks[k] = 0;
+        rank[k] = -1;
+        if (comm && p->comms[k]) {
+            if (ncclCommCount(p->comms[k], nranks + k) != ncclSuccess ||
+                ncclCommUserRank(p->comms[k], rank + k) != ncclSuccess)
+                return fail("ncclCommCount / ncclCommUserRank failed for replica %d", k);
+        }
+    }
     return 0;
 }
 

@@ -84,12 +84,16 @@ TORJ_HD cplx operator-(cplx a, double s) { return {a.re - s, a.im}; }
 TORJ_HD cplx I_times(cplx a) { return {-a.im, a.re}; }
 TORJ_HD double cabs_(cplx a) { return hypot(a.re, a.im); }
 TORJ_HD double cnorm_(cplx a) { return fma(a.re, a.re, a.im * a.im); }  // |a|^2
-// principal branch, as Julia's sqrt(::ComplexF64), for the moderate operands of
-// warmdisp (|z| within 1e+-150: |z| from the sum of squares without hypot's
-// scaling, one reciprocal instead of two divisions; ~1 ulp)
+// principal branch, as Julia's sqrt(::ComplexF64): for the moderate operands of
+// warmdisp (|z|^2 a normal double) |z| from the sum of squares without hypot's
+// scaling, one reciprocal instead of two divisions (~1 ulp); where |z|^2
+// underflows to 0 / a subnormal or overflows (|z| beyond ~1e-154 .. 1e154, e.g.
+// the discriminant near mode coupling) |z| by hypot, as before -- one compare,
+// almost never taken
 TORJ_HD cplx csqrt_(cplx z) {
     if (z.re == 0.0 && z.im == 0.0) return {0.0, z.im};
-    const double r = sqrt_nn(cnorm_(z));
+    const double n2 = cnorm_(z);
+    const double r = (n2 >= 0x1p-1022 && n2 < INFINITY) ? sqrt_nn(n2) : hypot(z.re, z.im);
     const double t = sqrt_nn(0.5 * (r + fabs(z.re))), h = 0.5 * rcp_nz(t);
     if (z.re >= 0.0) return {t, z.im * h};
     return {fabs(z.im) * h, copysign(t, z.im)};

@@ -19,7 +19,7 @@ module TorJHIP
 import TorJ
 
 const libtorj = get(ENV, "TORJ_HIP_LIB", joinpath(@__DIR__, "..", "build", "libtorj_hip.so"))
-const ABI_VERSION = 7  # include/torj_hip.h TORJ_ABI_VERSION
+const ABI_VERSION = 8  # include/torj_hip.h TORJ_ABI_VERSION
 
 function __init__()
     v = ccall((:torj_abi_version, libtorj), Cint, ())

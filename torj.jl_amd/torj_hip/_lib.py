@@ -95,6 +95,7 @@ _SIGS = {
     "torj_timing": (C.c_int, [C.c_void_p, C.c_int]),
     "torj_timing_read": (C.c_int, [C.c_void_p, _ip, _dp, _dp]),
     "torj_beam_timing_read": (C.c_int, [C.c_void_p, C.c_int, _ip, _dp, _dp, _dp]),
+    "torj_beam_comm_info": (C.c_int, [C.c_void_p, C.c_int, _ip, _ip, _ip]),
     "torj_trace_device": (C.c_int, [C.c_void_p, C.POINTER(TraceCfg), C.c_int, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -107,7 +108,7 @@ _SIGS = {
 }
 
 EXPORTED = tuple(_SIGS)
-ABI_VERSION = 7  # include/torj_hip.h TORJ_ABI_VERSION
+ABI_VERSION = 8  # include/torj_hip.h TORJ_ABI_VERSION
 
 _lib = None
 

@@ -62,3 +62,16 @@ def trace_beam_device(plasma, cfg, n_psi: int, shards) -> None:
                 v = v.data_ptr()
             setattr(arr[k], f, v)
     check(lib().torj_trace_beam_device(plasma.handle, C.byref(cfg), len(shards), int(n_psi), arr))
+
+
+def beam_comm_info(plasma, n_gpus: int) -> dict:
+    """torj_beam_comm_info: per replica of the last fan-out over n_gpus, the HIP
+    device it ran on and its RCCL communicator's rank count and rank
+    (ncclCommCount / ncclCommUserRank; 0 / -1 without a communicator: one
+    replica, or the test-only same-device placement)."""
+    from ._lib import check, lib
+    import ctypes as C
+
+    dev, nr, rk = (C.c_int * n_gpus)(), (C.c_int * n_gpus)(), (C.c_int * n_gpus)()
+    check(lib().torj_beam_comm_info(plasma.handle, int(n_gpus), dev, nr, rk))
+    return {"device": list(dev), "rccl_nranks": list(nr), "rccl_rank": list(rk)}
