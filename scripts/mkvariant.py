@@ -9,8 +9,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 name = sys.argv[1]
-flags = [a for a in sys.argv[2:] if a.startswith("-D")]
-specs = [a for a in sys.argv[2:] if not a.startswith("-D")]
+flags = [a for a in sys.argv[2:] if a.startswith("-")]
+specs = [a for a in sys.argv[2:] if not a.startswith("-")]
 base = f"/tmp/torj_variant/{name}"
 shutil.rmtree(base, ignore_errors=True)
 shutil.copytree(os.path.join(ROOT, "torj.jl_amd", "csrc"), f"{base}/pkg/csrc")

@@ -2,7 +2,9 @@
 """Lane utilisation of the Albajar alpha kernel (k_alpha_pts) on the C3 beam:
 a profiling build (python scripts/mkvariant.py aprof -DTORJ_ALPHA_PROF) counts,
 per harmonic, the waves that run the node loop and the lanes of those waves
-that need it, and the waves / live lanes of the kernel.
+that need it, the waves / live lanes of the kernel, and the waves that reach
+each region of abs_albajar_fast_body (Te >= 20, the polarisation prologue,
+each harmonic past its exact-zero test and its skip bound).
 usage: TORJ_HIP_LIB=.../libtorj_hip_aprof.so python tools/alpha_prof.py"""
 import ctypes
 import json
@@ -32,7 +34,7 @@ def main():
                                             s["inverse_curvature_radius"], f, N_rings=92,
                                             min_azimuthal_points=11)
     xp, Np, s0, st = T.ray_entry(P, pos, dirs, om, 1, gpu=True)
-    buf = (ctypes.c_ulonglong * 8)()
+    buf = (ctypes.c_ulonglong * 16)()
     T.trace(P, xp, Np, om, 1, ds=1e-4, n_steps=2000)
     rd(buf)
     T.trace(P, xp, Np, om, 1, ds=1e-4, n_steps=2000)
@@ -45,6 +47,11 @@ def main():
         out[f"harmonic{m}"] = {"node_loop_waves": wv, "node_loop_lanes": ln,
                                "lane_utilisation": ln / max(64 * wv, 1),
                                "waves_per_kernel_wave": wv / max(v[4], 1)}
+    # waves that reached each region of abs_albajar_fast_body (per kernel wave)
+    names = ["te_ge_20", "polarisation_prologue", "prologue_ok", "h2_not_zero", "h2_bound",
+             "h3_not_zero", "h3_bound"]
+    out["region_waves"] = {nm: v[6 + k] for k, nm in enumerate(names)}
+    out["region_waves_per_kernel_wave"] = {nm: v[6 + k] / max(v[4], 1) for k, nm in enumerate(names)}
     print(json.dumps(out, indent=1))
 
 

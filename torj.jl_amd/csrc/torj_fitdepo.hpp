@@ -599,7 +599,10 @@ TORJ_HD void fit_depo_ray(const FitArgs &a, int i, double psiL) {
 // window (m < kDepoQ + kDepoW + 5) is exactly fit_depo_ray.  Against the one
 // global elimination the second derivatives move by rounding only (the window
 // start's influence is ~5e-19 where it is used).
-constexpr int kDepoQ = 64, kDepoW = 32;
+#ifndef TORJ_DEPO_Q  // segments per streamed window
+#define TORJ_DEPO_Q 64
+#endif
+constexpr int kDepoQ = TORJ_DEPO_Q, kDepoW = 32;
 // one ray's walk between launches, SoA [field][n]
 enum { kDsFhi, kDsFlo, kDsOF0, kDsOF1, kDsMl, kDsMr, kDsMn, kDsMPl, kDsMPr, kDsMPn, kDsYl, kDsPl, kDsNd };
 enum { kDsJ, kDsC, kDsOQ0, kDsOQ1, kDsSpill, kDsRk0, kDsRk1, kDsRd, kDsRuns, kDsLast, kDsNi };

@@ -37,6 +37,23 @@
 
 using namespace torj;
 
+// The split pipeline's trajectory kernel k_traj_cell is compiled in its own
+// translation unit (torj_traj.hip, which includes this file up to the
+// trajectory kernels with TORJ_TRAJ_TU defined) without machine-level loop-
+// invariant code motion: hoisted out of the step loop, the kernel arguments'
+// loads and constants held 208 VGPRs and spilled 15 SGPRs; left in place, 160
+// VGPRs and no spill, so two trajectory waves and two 80-VGPR alpha waves share
+// a SIMD.  The alpha kernel keeps the hoisting (without
+// it +3.4 % VALU and +49 % SALU).  That TU's device globals are its own copies.
+#ifndef TORJ_TRAJ_OWN_TU  // 1 (the Makefile): k_traj_cell comes from torj_traj.hip
+#define TORJ_TRAJ_OWN_TU 0
+#endif
+#ifdef TORJ_TRAJ_TU
+#define TORJ_TU_LOCAL static
+#else
+#define TORJ_TU_LOCAL
+#endif
+
 // ===========================================================================
 // error handling
 // ===========================================================================
@@ -61,7 +78,7 @@ static int fail(const char *fmt, ...) {
 // ===========================================================================
 // Gauss-Legendre table in constant memory (abs_Al_init, src/absorption.jl:1-7)
 // ===========================================================================
-__constant__ GLTable c_gl;
+TORJ_TU_LOCAL __constant__ GLTable c_gl;
 
 static std::mutex g_gl_mu;
 static GLTable g_gl_host;
@@ -446,7 +463,7 @@ __global__ void __launch_bounds__(TORJ_BLOCK, TORJ_MIN_WAVES) k_trace(TraceArgs 
 // algorithm (oracle/torj_oracle.c ts_ray); parity with DiffEq is unpinned.
 // The seven stage vectors live in LDS (7 x 7 x 64 lanes x 8 B = 25 KB/wave).
 // ---------------------------------------------------------------------------
-__constant__ double c_ts_a[7][6] = {
+TORJ_TU_LOCAL __constant__ double c_ts_a[7][6] = {
     {0, 0, 0, 0, 0, 0},
     {0.161, 0, 0, 0, 0, 0},
     {-0.008480655492356989, 0.335480655492357, 0, 0, 0, 0},
@@ -456,7 +473,7 @@ __constant__ double c_ts_a[7][6] = {
      -0.028269050394068383, 0},
     {0.09646076681806523, 0.01, 0.4798896504144996, 1.379008574103742, -3.290069515436081,
      2.324710524099774}};
-__constant__ double c_ts_bt[7] = {-0.00178001105222577714, -0.0008164344596567469,
+TORJ_TU_LOCAL __constant__ double c_ts_bt[7] = {-0.00178001105222577714, -0.0008164344596567469,
                                   0.007880878010261995,    -0.1447110071732629,
                                   0.5823571654525552,      -0.45808210592918697,
                                   0.015151515151515152};
@@ -1280,10 +1297,18 @@ __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) k_traj_tile(TraceArg
 #else
 #define TORJ_TRAJ_CELL_ATTR
 #endif
+#if defined(TORJ_TRAJ_TU) || !TORJ_TRAJ_OWN_TU
 template <int DEPO, bool TRAJ>
 __global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) TORJ_TRAJ_CELL_ATTR k_traj_cell(TraceArgs a, SplitArgs sp) {
     traj_body<DEPO, TRAJ, kTrajCell>(a, sp);
 }
+#else
+// defined and instantiated in torj_traj.hip (its own compile flags, above)
+template <int DEPO, bool TRAJ>
+__global__ void __launch_bounds__(64, TORJ_TRAJ_TILE_WAVES) TORJ_TRAJ_CELL_ATTR k_traj_cell(TraceArgs a, SplitArgs sp);
+#endif
+
+#ifndef TORJ_TRAJ_TU  // the rest of the library (torj_traj.hip stops here)
 
 // alpha at the stored stage points of one block: block = kAlphaBlock lanes
 // (TORJ_ALPHA_BLOCK, default 128: two groups of 64 rays) at one (step j,
@@ -1348,6 +1373,71 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     } else {
         sp.alpha[(size_t)js * a.n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
             c_gl, a.omega, X, Y, Nabs, Npar, Te, a.mode, nullptr, 0, c_gl.tiny_alpha);
+    }
+}
+
+// k_alpha_pts with each workgroup taking P consecutive (step, stage) points of
+// its rays (TORJ_ALPHA_PPW = P > 1, a measurement variant): the kernel's per-wave
+// setup (arguments, the 2-D index, the rays' stop words) once per P points, and
+// the next point's five inputs loaded while the current one is evaluated.  The
+// lanes of a wave at one point are the same rays as k_alpha_pts' wave there, so
+// the Bessel-level ballot and every alpha are the same bits.
+#ifndef TORJ_ALPHA_PPW
+#define TORJ_ALPHA_PPW 1
+#endif
+#ifndef TORJ_ALPHA_PREFETCH
+#define TORJ_ALPHA_PREFETCH 1
+#endif
+template <bool COUNT, int P>
+__global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts_mp(TraceArgs a, SplitArgs sp, int nq) {
+    const int i = blockIdx.x * kAlphaBlock + threadIdx.x;
+    if (i >= a.n) return;
+    const int js0 = blockIdx.y * P;
+    const int np = min(P, 4 * sp.kb - js0);  // workgroup-uniform
+    const int ti = sp.tinfo[i], si = sp.sinfo[i];
+    // the ray's last stored point + 1 (0 when the scan has stopped it: sinfo may
+    // be stale, an optimisation only, as in k_alpha_pts)
+    const int js_end = info_status(si) != ST_OK ? 0 : 4 * (info_steps(ti) - sp.k0);
+    const size_t n = (size_t)a.n, stride = (size_t)sp.nf * n;
+    const double *in = sp.ain + (size_t)js0 * stride + i;
+    double X = in[0], Y = in[n], N2 = in[2 * n], Npar = in[3 * n], lnTe = in[4 * n];
+    for (int p = 0; p < np; p++) {
+        const int js = js0 + p;
+        // the quadrature table's address laundered per point: its loads (and the
+        // address arithmetic) stay inside the loop instead of being hoisted into
+        // registers live across the whole body (hundreds of SGPR spills otherwise)
+        const GLTable *glp = &c_gl;
+        asm volatile("" : "+s"(glp));
+#if TORJ_ALPHA_PREFETCH
+        double Xn = 0.0, Yn = 0.0, N2n = 0.0, Nparn = 0.0, lnTen = 0.0;
+        if (p + 1 < np) {  // the next point's inputs in flight during this one
+            const double *nx = in + (size_t)(p + 1) * stride;
+            Xn = nx[0], Yn = nx[n], N2n = nx[2 * n], Nparn = nx[3 * n], lnTen = nx[4 * n];
+        }
+#endif
+        if (js < js_end) {
+            const double Nabs = TORJ_AIN_TRAJ_MATH ? N2 : sqrt_pos(N2),
+                         Te = TORJ_AIN_TRAJ_MATH ? lnTe : exp_fast<true>(lnTe);
+            if constexpr (COUNT) {
+                AlbajarWork work = {};
+                sp.alpha[(size_t)js * n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
+                    *glp, a.omega, X, Y, Nabs, Npar, Te, a.mode, &work, 0, glp->tiny_alpha);
+                sp.awork[(size_t)js * n + i] = (work.n_active & 1u) | ((work.n_harm & 3u) << 1) |
+                                               ((work.n_zero & 3u) << 3) | (min(work.n_terms, 2047u) << 5) |
+                                               ((work.n_negl & 3u) << 16) | ((work.n_early & 3u) << 18);
+            } else {
+                sp.alpha[(size_t)js * n + i] = abs_albajar_fast_body<1, TORJ_ALPHA_UNROLL>(
+                    *glp, a.omega, X, Y, Nabs, Npar, Te, a.mode, nullptr, 0, glp->tiny_alpha);
+            }
+        }
+#if TORJ_ALPHA_PREFETCH
+        X = Xn, Y = Yn, N2 = N2n, Npar = Nparn, lnTe = lnTen;
+#else
+        if (p + 1 < np) {
+            const double *nx = in + (size_t)(p + 1) * stride;
+            X = nx[0], Y = nx[n], N2 = nx[2 * n], Npar = nx[3 * n], lnTe = nx[4 * n];
+        }
+#endif
     }
 }
 
@@ -2289,7 +2379,20 @@ static int ensure_split(torj_plasma_s *p, size_t bytes) {
         } else {
             HIPCK(hipStreamCreateWithPriority(&p->streamT, hipStreamNonBlocking, stream_prio("TORJ_TRAJ_PRIO", hi, lo, hi)));
             HIPCK(hipStreamCreateWithPriority(&p->stream2, hipStreamNonBlocking, stream_prio("TORJ_ALPHA_PRIO", lo, lo, hi)));
-            HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, stream_prio("TORJ_SCAN_PRIO", lo, lo, hi)));
+            // TORJ_SCAN_CUS=Z (measurement knob): the scan's stream -- the optical-depth
+            // scan and the streamed deposition's elimination and walk, latency-bound
+            // waves of up to 168 VGPRs -- on Z evenly spread CUs only, so the others
+            // keep their registers for the alpha waves
+            const char *sc = getenv("TORJ_SCAN_CUS");
+            const int Z = sc ? atoi(sc) : 0;
+            if (Z > 0 && Z < ncu) {
+                std::vector<uint32_t> mS((ncu + 31) / 32, 0u);
+                for (int c = 0; c < ncu; c++)
+                    if (((long)(c + 1) * Z) / ncu != ((long)c * Z) / ncu) mS[c / 32] |= 1u << (c % 32);
+                HIPCK(hipExtStreamCreateWithCUMask(&p->streamS, (uint32_t)mS.size(), mS.data()));
+            } else {
+                HIPCK(hipStreamCreateWithPriority(&p->streamS, hipStreamNonBlocking, stream_prio("TORJ_SCAN_PRIO", lo, lo, hi)));
+            }
         }
         for (int q = 0; q < torj_plasma_s::kRing; q++) {
             HIPCK(hipEventCreateWithFlags(&p->ev_T[q], hipEventDisableTiming));
@@ -2445,7 +2548,7 @@ const char *torj_build_id(void) { return TORJ_BUILD_ID; }
 int torj_alpha_prof_read(unsigned long long *out) {
     HIPCK(hipDeviceSynchronize());
     HIPCK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_aprof), sizeof(g_aprof)));
-    static const unsigned long long zero[8] = {};
+    static const unsigned long long zero[16] = {};
     HIPCK(hipMemcpyToSymbol(HIP_SYMBOL(g_aprof), zero, sizeof(g_aprof)));
     return 0;
 }
@@ -3202,10 +3305,20 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             else TORJ_WARM_LAUNCH(1, false);
         }
 #undef TORJ_WARM_LAUNCH
+#if TORJ_ALPHA_PPW > 1
+        else {
+            const dim3 agridP((unsigned)nqA, (unsigned)((4 * sp.kb + TORJ_ALPHA_PPW - 1) / TORJ_ALPHA_PPW));
+            if (sp.awork)
+                hipLaunchKernelGGL((k_alpha_pts_mp<true, TORJ_ALPHA_PPW>), agridP, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
+            else
+                hipLaunchKernelGGL((k_alpha_pts_mp<false, TORJ_ALPHA_PPW>), agridP, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
+        }
+#else
         else if (sp.awork)  // a counted launch
             hipLaunchKernelGGL(k_alpha_pts<true>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
         else
             hipLaunchKernelGGL(k_alpha_pts<false>, agridA, dim3(kAlphaBlock), 0, s2, a, sp, nqA);
+#endif
         HIPCK(hipEventRecord(p->ev_A[r], s2));
         if (s3 != s2) HIPCK(hipStreamWaitEvent(s3, p->ev_A[r], 0));
         if (a.counters)
@@ -3221,9 +3334,15 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         if (dstream && !depo_traj && b + 1 < n_blocks) {
             if (depo_own) HIPCK(hipStreamWaitEvent(sD, p->ev_S[r], 0));
             if (dstream_env == 3 || dstream_env == 4) {  // elimination and walk as two launches
-                hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sD, *fa, ds, sp.sinfo, sp.k0 + sp.kb);
-                hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
-                                   sp.k0 + sp.kb);
+                // each pair advances a ray by at most one window of kDepoQ
+                // segments, so a block of more steps than that takes as many pairs
+                // as it has windows (blocks of 120 steps: two), and the walk keeps
+                // up with the scan instead of leaving windows for k_depo_tail
+                for (int w = 0; w < (sp.kb + kDepoQ - 1) / kDepoQ; w++) {
+                    hipLaunchKernelGGL(k_depo_elim, dim3(G), dim3(64), 0, sD, *fa, ds, sp.sinfo, sp.k0 + sp.kb);
+                    hipLaunchKernelGGL(k_depo_walk, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
+                                       sp.k0 + sp.kb);
+                }
             } else {
                 hipLaunchKernelGGL(k_depo_stream, dim3(G), dim3(64), fit_lds, sD, *fa, ds, sp.sinfo,
                                    sp.k0 + sp.kb);
@@ -4381,3 +4500,5 @@ int torj_trace_check(torj_plasma_t p, void *stream) {
 }
 
 }  // extern "C"
+
+#endif  // TORJ_TRAJ_TU

@@ -238,6 +238,19 @@ TORJ_HD double exp2_node(double y) {
 #endif
 }
 
+// x 2^k (v_ldexp_f64 on the device)
+TORJ_HD double ldexp_i(double x, int k) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_ldexp(x, k);
+#else
+    return ldexp(x, k);
+#endif
+}
+#ifndef TORJ_EMAX_BOUND  // albajar_harmonic's skip tests: E_max by a power-of-two bound (1, round 6:
+// C3 trace phase 40.28 / 40.29 -> 39.77 / 39.86 ms alternating) or by exp (0)
+#define TORJ_EMAX_BOUND 1
+#endif
+
 // Stencil position on one axis: clamped coordinate, cell index, weights.
 struct Axis {
     int i;
@@ -1170,8 +1183,25 @@ TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, doub
 
 #ifdef TORJ_ALPHA_PROF
 // profiling build only (tools/alpha_prof.py): [2 (m - 2)] waves and [2 (m - 2) + 1]
-// lanes that ran harmonic m's node loop, [4] waves and [5] live lanes of k_alpha_pts
-__device__ unsigned long long g_aprof[8];
+// lanes that ran harmonic m's node loop, [4] waves and [5] live lanes of k_alpha_pts;
+// [6 ..] waves that reached a region of abs_albajar_fast_body (kAprof*)
+enum { kAprofTe = 6, kAprofPro, kAprofOk, kAprofH2, kAprofB2, kAprofH3, kAprofB3, kAprofN = 13 };
+#ifdef TORJ_TRAJ_TU
+static
+#endif
+__device__ unsigned long long g_aprof[16];
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TORJ_APROF_WAVE(K)                                                          \
+    do {                                                                            \
+        const unsigned long long am_ = __ballot(1);                                 \
+        if ((int)__lane_id() == __builtin_ffsll((long long)am_) - 1) atomicAdd(&g_aprof[K], 1ull); \
+    } while (0)
+#endif
+#endif
+#ifndef TORJ_APROF_WAVE
+#define TORJ_APROF_WAVE(K) \
+    do {                   \
+    } while (0)
 #endif
 
 // Work counters of one lane (include/torj_hip.h torj_trace: counters[2..7]).
@@ -1235,6 +1265,7 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
         if (work) work->n_zero++;
         return -mu * Pm * Pm * 0.0 * sq_r;
     }
+    TORJ_APROF_WAVE(M == 2 ? kAprofH2 : kAprofH3);
     // Negligible next to the harmonics already summed (dom = their sum so far,
     // abs_albajar_fast_body adds this one to it next): when a rigorous bound B
     // on |this integral| is below 2^-58 |dom|, dom + h rounds to dom exactly
@@ -1256,6 +1287,7 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     // tau by less than 2 tiny_alpha per metre of ray.
     const bool rel = gl.negl_skip && dom != 0.0 && fabs(dom) < INFINITY && fabs(dom) > 1e-290;
     if (rel || hmax > 0.0) {
+        TORJ_APROF_WAVE(M == 2 ? kAprofB2 : kAprofB3);
         constexpr double iS = inv_fact(M), iS1 = inv_fact(M + 1), iSl = inv_fact(M - 1);
         const double hx = c.hx, hx2 = hx * hx;
         const double A = hx * (iS * iS), T1 = hx2 * iS1;
@@ -1267,7 +1299,18 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
         for (int k = 1; k < 2 * M - 1; k++) p *= hx;
         const double B0 = 4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax);
         const double R = B0 * rcp_nz(fabs(dom));
+#if TORJ_EMAX_BOUND
+        // an upper bound on E_max = exp(mu (1 - gamma_min)) without the exponential:
+        // 2^(ceil(y) + 1) with y = mu log2(e) (1 - gamma_min) from the node loop's
+        // square root (a few ulp; the extra factor 2 covers y's rounding, |y| <
+        // 2^16), so the bound stays rigorous with at most 4x of slack; a NaN y
+        // gives an infinite bound (fmin / fmax return the non-NaN operand), which
+        // never skips
+        const double yb = ceil(c.mu2 * (1.0 - sqrt_node(qmin))) + 1.0;
+        const double Emax = ldexp_i(1.0, (int)fmax(fmin(yb, 2000.0), -2000.0));
+#else
         const double Emax = exp_fast<true>(mu * (1.0 - sqrt_nn(qmin)));
+#endif
         // R, B0 < 1e300: an E_max that underflowed to 0 cannot hide a huge bound
         if ((rel && R < 1e300 && R * Emax < 0x1p-58) || (B0 < 1e300 && B0 * Emax < hmax)) {
             if (work) work->n_negl++;
@@ -1450,6 +1493,7 @@ TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, 
                                      double N_abs, double N_par, double Te, int mode,
                                      AlbajarWork *work, int sub = 0, double tiny = 0.0) {
     if (Te < 20.0) return 0.0;
+    TORJ_APROF_WAVE(kAprofTe);
     const AlbPre pre = albajar_pre(Y, N_abs, N_par, Te);
     const bool h2 = !(2.0 < pre.m_0), h3 = !(3.0 < pre.m_0);  // harmonic m present iff m >= m_0
     HarmGeom g2{}, g3{};
@@ -1469,8 +1513,10 @@ TORJ_HD double abs_albajar_fast_body(const GLTable &gl, double omega, double X, 
         if (work) work->n_early += (uint32_t)h2 + (uint32_t)h3;
         return 0.0;
     }
+    TORJ_APROF_WAVE(kAprofPro);
     const AlbPro q = albajar_prologue(pre, X, Y, N_abs, N_par, mode);
     if (!q.ok) return 0.0;
+    TORJ_APROF_WAVE(kAprofOk);
     if (work) work->n_active++;
     const double hmax = tiny_harmonic(tiny, q, X, omega);
     double c_abs = 0.0;

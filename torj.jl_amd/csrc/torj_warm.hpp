@@ -23,7 +23,13 @@ namespace torj {
 // per workgroup), k_alpha_warm_pts flushes them once per wave.
 #ifdef TORJ_WARM_PROF
 constexpr int kWProfN = 8;
+#ifdef TORJ_TRAJ_TU
+static
+#endif
 __device__ unsigned long long g_wprof[kWProfN + 1];
+#ifdef TORJ_TRAJ_TU
+static
+#endif
 __device__ unsigned long long g_wfad[9];  // faddeeva_upper2's branch statistics (see there)
 #endif
 #if defined(TORJ_WARM_PROF) && defined(__HIP_DEVICE_COMPILE__)
