@@ -183,7 +183,15 @@ def main():
                           args.n_steps * args.ds, 100)
     d_xl, d_s0 = dev_t(pos.T), dev_t(s0)
     L = T.lib()
-    stream = torch.cuda.current_stream(dev)
+    # the hot path's caller stream: a stream of its own (non-blocking, like the
+    # library's internal ones), made torch's current stream so that the per-step
+    # zeroing runs on it too; TORJ_BENCH_STREAM=default keeps torch's default
+    # (legacy NULL) stream, which synchronises implicitly with blocking streams
+    if os.environ.get("TORJ_BENCH_STREAM", "own") == "default":
+        stream = torch.cuda.current_stream(dev)
+    else:
+        stream = torch.cuda.Stream(device=dev)
+        torch.cuda.set_stream(stream)
 
     def launch(counters=None):
         d_dP.zero_()
