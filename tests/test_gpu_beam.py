@@ -316,3 +316,44 @@ def test_c4_million_ray_beam_sharded_rccl_batched(gpu, T, hplasma, oplasma):
     # make_beam's deposited power (normalised weights): most of the beam power is
     # absorbed in the X2 layer, though the 291-ring fan's outer rings miss it
     assert 0.5 < b.dP_shell[-1] <= 1.0 + 1e-12
+
+
+@pytest.mark.parametrize("sched", [3, 1])
+def test_trace_device_null_stream_equals_explicit_stream(gpu, T, hplasma, sched):
+    """torj_trace_device_ex on the legacy NULL stream -- served on the handle's
+    own non-blocking stream with fork / join events against it -- equals the
+    same call on an explicit stream bit for bit (the split pipeline, sched 3,
+    and the work queue, sched 1), and the outputs are complete when the NULL
+    stream is synchronised."""
+    import torch
+
+    from torj_hip._lib import TraceCfg
+
+    pos, xp, Np, s0, w, om = _beam(T, hplasma)
+    n = len(w)
+    grid = np.linspace(0, 1, 200)
+    cfg = TraceCfg(om, 1, 1e-4, 600, 20, 1.0, 1e-6, 1, 100, 1)
+    dev = torch.device("cuda", 0)
+    outs = []
+    try:
+        hplasma.set_sched(sched)
+        for explicit in (False, True):
+            sh = _device_shards(torch, T, hplasma, cfg, len(grid), grid, xp, Np, w, pos, s0,
+                                [slice(0, n)], dev)[0]
+            torch.cuda.synchronize()
+            st = torch.cuda.Stream(device=dev) if explicit else None
+            T._lib.check(T.lib().torj_trace_device_ex(
+                hplasma.handle, cfg, n, sh["x0"].data_ptr(), sh["N0"].data_ptr(), sh["weights"].data_ptr(),
+                len(grid), sh["psi_grid"].data_ptr(), sh["x_launch"].data_ptr(), sh["s0"].data_ptr(),
+                sh["state"].data_ptr(), sh["status"].data_ptr(), sh["steps"].data_ptr(),
+                sh["dP_shell"].data_ptr(), sh["P_dep"].data_ptr(), sh["traj"].data_ptr(), None,
+                st.cuda_stream if explicit else None))
+            T._lib.check(T.lib().torj_trace_check(hplasma.handle, st.cuda_stream if explicit else None))
+            outs.append({k: sh[k].cpu().numpy() for k in ("state", "status", "steps", "dP_shell", "P_dep", "traj")})
+    finally:
+        hplasma.set_sched(-1)
+    a, b = outs
+    assert (a["steps"] > 0).all()
+    for k in ("state", "status", "steps", "dP_shell", "P_dep"):
+        assert np.array_equal(a[k], b[k]), k
+    assert np.array_equal(a["traj"], b["traj"], equal_nan=True)

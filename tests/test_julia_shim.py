@@ -136,7 +136,7 @@ def test_shim_parses_every_ccall():
     # the shim's entry points of the drop-in (make_ray / make_beam path)
     for s in ("torj_abi_version", "torj_plasma_create", "torj_plasma_create_from_coefs",
               "torj_ray_entry_gpu", "torj_trace_beam", "torj_launch_peripheral_rays",
-              "torj_shell_volumes", "torj_abs_al_init", "torj_alpha_warm"):
+              "torj_shell_volumes", "torj_abs_al_init", "torj_alpha_warm", "torj_beam_comm_info"):
         assert s in syms, s
 
 

@@ -429,20 +429,54 @@ constexpr double dfact_odd(int k) {  // (2k - 1)!!, (-1)!! = 1: exact below 2^53
     return f;
 }
 TORJ_HD bool faddeeva_asym_ok(double x, double y) { return fabs(x) >= kFadAsym || y >= kFadAsym; }
-TORJ_HD cplx faddeeva_asym(double x, double y) {
-    constexpr double kInvSqrtPi = 0.56418958354775628695;
-    const double ir2 = rcp_nz(fma(x, x, y * y));
-    const double a = x * ir2, b = -y * ir2;  // 1 / z
-    const double ur = 0.5 * fma(a, a, -b * b), ui = a * b;  // u = (1 / z)^2 / 2
-    // T = sum_{k < K} (2k - 1)!! u^k by Horner with the double factorials as
-    // constants (4 VALU per term; the nested 1 + (2j - 1) u (...) form took 6)
-    double tr = dfact_odd(kFadAsymK - 1), ti = 0.0;
+// T = sum_{k < K} (2k - 1)!! u^k by Horner with the double factorials as
+// constants (4 VALU per term; the nested 1 + (2j - 1) u (...) form took 6)
+template <int K>
+TORJ_HD void asym_horner(double ur, double ui, double &tr, double &ti) {
+    tr = dfact_odd(K - 1), ti = 0.0;
 #pragma unroll
-    for (int k = kFadAsymK - 2; k >= 0; k--) {  // T = T u + (2k - 1)!!
+    for (int k = K - 2; k >= 0; k--) {  // T = T u + (2k - 1)!!
         const double t = fma(tr, ur, fma(-ti, ui, dfact_odd(k)));
         ti = fma(tr, ui, ti * ur);
         tr = t;
     }
+}
+// The series' length (TORJ_FAD_ASYM_ADAPT): the fewest terms K whose first
+// omitted term (2K - 1)!! / (2 |z|^2)^K is at most 2^-56 of the leading 1, for
+// the smallest |z|^2 the wave evaluates (wave-uniform on the device, so the
+// Horner chain does not diverge): |z|^2 >= 0.5 ((2K - 1)!! 2^56)^(1/K), i.e.
+// 10 terms from |z|^2 = 256 (the branch's edge), 9 from 256.9, 8 from 393.2,
+// 7 from 692.2, 6 from 1506.9, 5 from 4630.2 (each threshold rounded up)
+#ifndef TORJ_FAD_ASYM_ADAPT
+#define TORJ_FAD_ASYM_ADAPT 0
+#endif
+TORJ_HD int asym_terms(double r2) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __ballot(r2 < 256.9) ? 10 : __ballot(r2 < 393.2) ? 9 : __ballot(r2 < 692.2) ? 8
+         : __ballot(r2 < 1506.9) ? 7 : __ballot(r2 < 4630.2) ? 6 : 5;
+#else
+    return r2 < 256.9 ? 10 : r2 < 393.2 ? 9 : r2 < 692.2 ? 8 : r2 < 1506.9 ? 7 : r2 < 4630.2 ? 6 : 5;
+#endif
+}
+TORJ_HD cplx faddeeva_asym(double x, double y) {
+    constexpr double kInvSqrtPi = 0.56418958354775628695;
+    const double r2 = fma(x, x, y * y);
+    const double ir2 = rcp_nz(r2);
+    const double a = x * ir2, b = -y * ir2;  // 1 / z
+    const double ur = 0.5 * fma(a, a, -b * b), ui = a * b;  // u = (1 / z)^2 / 2
+    double tr, ti;
+#if TORJ_FAD_ASYM_ADAPT
+    switch (asym_terms(r2)) {
+        case 5: asym_horner<5>(ur, ui, tr, ti); break;
+        case 6: asym_horner<6>(ur, ui, tr, ti); break;
+        case 7: asym_horner<7>(ur, ui, tr, ti); break;
+        case 8: asym_horner<8>(ur, ui, tr, ti); break;
+        case 9: asym_horner<9>(ur, ui, tr, ti); break;
+        default: asym_horner<kFadAsymK>(ur, ui, tr, ti); break;
+    }
+#else
+    asym_horner<kFadAsymK>(ur, ui, tr, ti);
+#endif
     const double pr = fma(a, tr, -b * ti), pim = fma(a, ti, b * tr);  // T / z
     cplx w;
     w.re = -kInvSqrtPi * pim;  // i T / (sqrt(pi) z)

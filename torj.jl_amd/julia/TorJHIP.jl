@@ -142,6 +142,16 @@ function trace(p::GPUPlasma, cfg::TraceCfg, x0::Matrix{Float64}, N0::Matrix{Floa
     return state, status, steps, dP, Pdep, traj
 end
 
+# who took part in the last make_beam reduce over n_gpus replicas (ABI 8): each
+# replica's HIP device and its RCCL communicator's rank count and rank (0 / -1
+# where no communicator exists)
+function beam_comm_info(p::GPUPlasma, n_gpus::Integer)
+    dev, nranks, rank = zeros(Cint, n_gpus), zeros(Cint, n_gpus), zeros(Cint, n_gpus)
+    check(ccall((:torj_beam_comm_info, libtorj), Cint,
+                (Ptr{Cvoid}, Cint, Ptr{Cint}, Ptr{Cint}, Ptr{Cint}), p.h, n_gpus, dev, nranks, rank))
+    return (device=dev, rccl_nranks=nranks, rccl_rank=rank)
+end
+
 function shell_volumes(p::GPUPlasma, g::Vector{Float64})
     dV = zeros(length(g) - 1)
     check(ccall((:torj_shell_volumes, libtorj), Cint, (Ptr{Cvoid}, Cint, Ptr{Float64}, Ptr{Float64}),
