@@ -18,7 +18,7 @@ O=gpurun_out/prof_$W
 mkdir -p $O/profiles profiles/$R
 bash scripts/profile.sh prof_$W $ARGS || exit 1
 python tools/prof_summary.py gpurun_out/prof_$W $O/profiles "k_traj|$ALPHA|k_tau_scan|k_split_final|k_depo_stream|k_depo_elim|k_depo_walk" $PRE || exit 1
-(cd /tmp && TORJ_SPLIT_SERIAL=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/serial -o s -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-host-api --steps 3 $ARGS > $GRAFT_REPO_ROOT/$O/serial.log 2>&1) || { echo serial failed; tail -5 $O/serial.log; exit 1; }
+(cd /tmp && TORJ_SPLIT_SERIAL=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/serial -o s -- python3 $GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-host-api --no-exact --steps 3 $ARGS > $GRAFT_REPO_ROOT/$O/serial.log 2>&1) || { echo serial failed; tail -5 $O/serial.log; exit 1; }
 f=$(find $O/serial -name '*kernel_stats.csv' | head -1); cp $f $O/profiles/${PRE}serial_kernel_stats.csv
 grep -E "k_traj|k_alpha|k_tau|k_depo|k_split" $f | cut -d, -f1-4
 cp $O/profiles/* profiles/$R/
