@@ -1,6 +1,6 @@
 """Build an A/B variant of libtorj_hip.so from a patched copy of the sources
 (profiling aid, never shipped): python scripts/mkvariant.py NAME [-DFLAG ...] 'file|||old|||new' ...
--> torj.jl_amd/build/variants/libtorj_hip_NAME.so (run by scripts/gpu_ab.sh); -D... arguments are
+-> torj.jl_amd/build/variants/libtorj_hip_NAME.so (run by scripts/gpu_call.sh AB=... or scripts/gpu_ab.sh); -D... arguments are
 extra compile flags (e.g. -DTORJ_WARM_PROF, the warm alpha's region timers: tools/warm_prof.py)."""
 import os
 import shutil
