@@ -92,3 +92,36 @@ def test_multi_gpu_line_schema():
     del bad["roofline"]
     with pytest.raises(KeyError):
         B.check_line(bad)
+
+
+def test_tiny_alpha_and_resolvable_tau_statistic(monkeypatch):
+    """config.tiny_alpha follows TORJ_TINY_ALPHA (default 1e-20), and the parity
+    object's unfloored tau statistic covers exactly the sampled rays with
+    tau_cpu >= 1e-12 (a tiny-tau ray with a large relative error does not count,
+    a resolvable one does)."""
+    import numpy as np
+
+    B = _bench_module()
+    monkeypatch.delenv("TORJ_TINY_ALPHA", raising=False)
+    assert B.tiny_alpha() == 1e-20 == B.TINY_ALPHA_DEFAULT
+    monkeypatch.setenv("TORJ_TINY_ALPHA", "0")
+    assert B.tiny_alpha() == 0.0
+
+    class Args:
+        absorption, mode, ds = "albajar", 1, 1e-4
+
+    n = 4
+    st = np.zeros((n, 7))
+    st[:, :3], st[:, 3:6] = [2.0, 0.1, 0.3], [0.5, 0.6, 0.1]
+    st[:, 6] = [1e-126, 3e-13, 2e-12, 0.5]
+    gpu = st.copy()
+    gpu[0, 6] = 0.0              # below any resolution: relative error 1, not counted
+    gpu[2, 6] *= 1 + 4e-11       # resolvable: counted
+    gpu[3, 6] *= 1 + 1e-12
+    r = {"state": st, "status": np.zeros(n, np.int32), "steps": np.full(n, 2000, np.int32)}
+    p = B._parity(None, r, np.arange(n), None, None, 0.0, Args,
+                  (gpu, np.zeros(n, np.int32), np.full(n, 2000, np.int32)), 1)
+    assert p["rays_tau_resolvable"] == 2 and p["tau_resolvable"] == 1e-12
+    assert abs(p["max_rel_tau_resolvable"] - 4e-11) < 1e-15
+    assert p["max_rel_tau_unfloored"] == 1.0
+    assert p["rays_within_bar"] == n  # the floored bar holds for all four
