@@ -223,4 +223,13 @@ void fe_eval(int nR, int nZ, double R1, double Rn, double Z1, double Zn, const d
         for (int q = 0; q < 4; q++) o[6 + 2 * q] = f.dR[q], o[7 + 2 * q] = f.dZ[q];
     }
 }
+#if defined(TORJ_ROOT_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+// statistics build only: cubic_root calls, Newton steps, histogram of steps per call
+void fd_root_stats(unsigned long long *out) {
+    out[0] = torj::g_root_calls, out[1] = torj::g_root_iters;
+    for (int k = 0; k < 8; k++) out[2 + k] = torj::g_root_hist[k];
+    torj::g_root_calls = torj::g_root_iters = 0;
+    for (int k = 0; k < 8; k++) torj::g_root_hist[k] = 0;
+}
+#endif
 }

@@ -215,13 +215,26 @@ struct Cursor {
     }
 };
 
+#if defined(TORJ_ROOT_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+// host statistics build only (tests/native): cubic_root calls and Newton steps
+inline unsigned long long g_root_calls = 0, g_root_iters = 0, g_root_hist[8] = {};
+#endif
 // root of the monotone cubic piece q(t) = L on [ta, tb], L strictly between
 // the end values: Newton with a bisection safeguard, to the last bit
 TORJ_HD double cubic_root(const Cubic &q, double L, double ta, double tb, double fa, double fb,
                           bool up) {
     double lo = ta, hi = tb, t = fma(L - fa, (tb - ta) * rcp_nz(fb - fa), ta);  // secant start
     if (!(t > lo && t < hi)) t = 0.5 * (ta + tb);
+#if defined(TORJ_ROOT_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+    struct Tally {
+        int it = 0;
+        ~Tally() { g_root_calls++, g_root_iters += it, g_root_hist[it < 7 ? it : 7]++; }
+    } tally;
+#endif
     for (int it = 0; it < 100; it++) {
+#if defined(TORJ_ROOT_STATS) && !defined(__HIP_DEVICE_COMPILE__)
+        tally.it = it + 1;
+#endif
         const double v = q.f(t) - L;
         if (v == 0.0) break;
         if ((v > 0.0) == up)
