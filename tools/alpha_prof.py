@@ -49,7 +49,7 @@ def main():
                                "waves_per_kernel_wave": wv / max(v[4], 1)}
     # waves that reached each region of abs_albajar_fast_body (per kernel wave)
     names = ["te_ge_20", "polarisation_prologue", "prologue_ok", "h2_not_zero", "h2_bound",
-             "h3_not_zero", "h3_bound"]
+             "h3_not_zero", "h3_bound", "zero_flag_waves"]
     out["region_waves"] = {nm: v[6 + k] for k, nm in enumerate(names)}
     out["region_waves_per_kernel_wave"] = {nm: v[6 + k] / max(v[4], 1) for k, nm in enumerate(names)}
     print(json.dumps(out, indent=1))

@@ -915,6 +915,8 @@ struct SplitArgs {
     int *tinfo;           // steps | status << 24: the trajectory kernel's stop (one store)
     double *stau, *spsi, *sPdep;  // the scan's carry
     int *sinfo;           // steps | status << 24: the scan's stop
+    unsigned char *zflag;  // per ray, this block (ring slot): 1 = Albajar alpha provably +-0 at every
+                           // stage point the trajectory kernel stored (zero_box_flag); null: off
     int k0, kb;           // block: steps [k0, k0 + kb)
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
     int tile_cap;         // k_traj_tile: most nodes a wave stages (<= kTileNodes)
@@ -935,6 +937,50 @@ __device__ __forceinline__ int info_steps(int v) { return v & 0xffffff; }
 __device__ __forceinline__ int info_status(int v) { return (unsigned)v >> 24; }
 __device__ __forceinline__ int make_info(int steps, int st) { return steps | (st << 24); }
 
+// The alpha-input box of one ray over a block (round 6): the range of ln Te,
+// Y, N_par^2 and N_perp^2 over every stage point the trajectory kernel stored.
+// zero_box_flag proves from it that abs_albajar_fast_body returns +-0 at every
+// one of them -- all Te < 20 eV, or each harmonic m = 2, 3 absent (m Y <
+// sqrt(1 - N_par^2)) or an exact zero (every node's exp(mu (1 - gamma))
+// underflows: gamma_min > 1 + 760 / mu, with gamma_min >= m Y / (1 + |N_par|)
+// on the resonance gamma - N_par u_par = m Y, |u_par| <= gamma) -- the early
+// settle of abs_albajar_fast_body (and its exact-zero test), which returns +0
+// there, decided for a whole block with relative margins of 1e-9 against
+// their roundings.  k_alpha_pts then writes 0 for a wave whose 64 rays all
+// carry the flag instead of evaluating it (42 % of its waves settle early on the
+// headline beam).
+struct ZBox {
+    double lte = -INFINITY, ylo = INFINITY, yhi = -INFINITY, np2 = -INFINITY, perp = INFINITY;
+    bool bad = false;
+};
+__device__ __forceinline__ void zero_box_add(ZBox &b, double lnTe, double Y, double Npar, double N2) {
+    const double np2 = Npar * Npar;
+    b.lte = fmax(b.lte, lnTe);
+    b.ylo = fmin(b.ylo, Y);
+    b.yhi = fmax(b.yhi, Y);
+    b.np2 = fmax(b.np2, np2);
+    b.perp = fmin(b.perp, fma(-1e-9, N2, N2 - np2));  // N_perp^2 with a relative margin
+    const double sum = lnTe + Y + Npar + N2;
+    b.bad |= !(sum == sum);  // a NaN input (fmin / fmax would drop it)
+}
+__device__ __forceinline__ bool zero_box_flag(const ZBox &b) {
+    if (b.bad) return false;
+    if (b.lte < 2.9957322735539909 - 1e-9) return true;  // every Te < 20 eV (ln 20)
+    if (!(b.ylo > 1e-200 && b.yhi < 1e200 && b.perp > 0.0 && b.np2 < 1.0 - 1e-9 && b.lte < 700.0))
+        return false;
+    constexpr double kMuTe = kMe * kC * kC / kE;  // mu Te (albajar_pre)
+    const double delta = 760.0 * (1.0 + 1e-9) * exp(b.lte) * (1.0 / kMuTe);  // 760 / mu_min
+    const double npm = sqrt(b.np2), sq = sqrt(1.0 - b.np2);
+    bool ok = true;
+#pragma unroll
+    for (int m = 2; m <= 3; m++) {
+        const bool absent = m * b.yhi * (1.0 + 1e-9) < sq * (1.0 - 1e-9);
+        const bool zero = m * b.ylo > (1.0 + delta) * (1.0 + npm) * (1.0 + 1e-9);
+        ok = ok && (absent || zero);
+    }
+    return ok;
+}
+
 #ifndef TORJ_AIN_TRAJ_MATH  // 1: the trajectory kernel stores |N| and Te for k_alpha_pts (not |N|^2, ln Te)
 #define TORJ_AIN_TRAJ_MATH 0
 #endif
@@ -947,7 +993,7 @@ template <bool STORE, int NS = kNF, class CS = const double *, bool PSI = false>
 __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
                                           const SplitArgs &sp, int j, int i, const double x[3],
                                           const double N[3], double xn[3], double Nn[3],
-                                          double *psi_x = nullptr) {
+                                          double *psi_x, ZBox &zb, bool zon) {
     const double hds = 0.5 * a.ds, ds6 = a.ds / 6.0;
     double acc[6] = {0, 0, 0, 0, 0, 0}, xt[3], Nt[3], k[6];
 #pragma unroll
@@ -975,6 +1021,7 @@ __device__ __forceinline__ bool cold_step(const TraceArgs &a, CS coef,
         if constexpr (STORE) {
             double *o = sp.ain + ((size_t)(j * 4 + st) * sp.nf) * a.n + i;
             const double N2 = Nt[0] * Nt[0] + Nt[1] * Nt[1] + Nt[2] * Nt[2];
+            if (zon) zero_box_add(zb, p.lnTe, p.Y, Npar, N2);
             o[0] = p.X;
             o[(size_t)a.n] = p.Y;
             o[3 * (size_t)a.n] = Npar;
@@ -1102,6 +1149,10 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
     };
     const int s_first = steps;
     bool pending = false;  // step steps - 1 still needs its psi
+    // (a value and a flag, not a pointer: a local behind a conditional pointer
+    // lived in scratch, 56 B per lane, and slowed the kernel by ~14 %)
+    ZBox zb;
+    const bool zon = sp.zflag != nullptr;
 #if defined(__HIP_DEVICE_COMPILE__) && TORJ_TRAJ_PREWAIT
     // every load before the step loop complete here (s_waitcnt vmcnt(0)): the
     // compiler otherwise waits at the loop header for the carry's loads, every
@@ -1111,7 +1162,7 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
 #endif
     for (int s = s_first; s < s_end; s++) {
         double xn[3], Nn[3], psi_x;
-        const bool bad = cold_step<true, NS, CS, true>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn, &psi_x);
+        const bool bad = cold_step<true, NS, CS, true>(a, coef, sp, s - sp.k0, i, x, N, xn, Nn, &psi_x, zb, zon);
         if (pending) {
             pending = false;
             if (step_end(s - 1, psi_x)) {
@@ -1158,6 +1209,7 @@ __device__ __forceinline__ void traj_run(const TraceArgs &a, const SplitArgs &sp
         sp.tx[(3 + c) * (size_t)a.n + i] = N[c];
     }
     sp.tinfo[i] = make_info(steps, st);
+    if (zon) sp.zflag[i] = zero_box_flag(zb) ? 1 : 0;
 }
 
 
@@ -1194,6 +1246,8 @@ __device__ __forceinline__ void traj_body(const TraceArgs &a, const SplitArgs &s
         // copy and the scan's carry).  Keep it that way: tests/test_gpu_split.py
         // test_split_serial_equals_overlapped holds both orders bit-identical.
         live = st == ST_OK && !(sp.k0 > 0 && info_status(sp.sinfo[i]) != ST_OK);
+        // a ray without trajectory steps in this block needs no alpha in it
+        if (!live && sp.zflag) sp.zflag[i] = 1;
     }
     if constexpr (MODE == kTrajTile) {
         // one wave per workgroup: the wave's live rays' (R, Z) box, widened by
@@ -1343,12 +1397,23 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     // row): the stop words and the inputs, whose addresses are valid for any
     // i < n whether or not the point is live
     const int ti = sp.tinfo[i], si = sp.sinfo[i];
+    const int zf = sp.zflag ? sp.zflag[i] : 0;
     const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
     const double X = in[0], Y = in[(size_t)a.n], N2 = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
     const double lnTe = in[4 * (size_t)a.n];
     // (an empty asm that consumes them: the compiler would otherwise sink the
     // input loads below the stop test and the Te test, three latencies in a row)
-    asm volatile("" ::"v"(ti), "v"(si), "v"(X), "v"(Y), "v"(N2), "v"(Npar), "v"(lnTe));
+    asm volatile("" ::"v"(ti), "v"(si), "v"(zf), "v"(X), "v"(Y), "v"(N2), "v"(Npar), "v"(lnTe));
+    // the trajectory kernel's block zero flags: a wave whose rays all carry one
+    // writes 0 (abs_albajar_fast_body's early settle returns +0 there) and ends
+    if (__all(zf != 0)) {
+#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
+        TORJ_APROF_WAVE(kAprofZ);
+#endif
+        sp.alpha[(size_t)js * a.n + i] = 0.0;
+        if constexpr (COUNT) sp.awork[(size_t)js * a.n + i] = 0u;
+        return;
+    }
     // sinfo may be stale (k_tau_scan of an earlier block runs on another
     // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
     // alpha the scan never reads
@@ -1542,14 +1607,15 @@ __global__ void __launch_bounds__(64) k_alpha_warm_big(TraceArgs a, SplitArgs sp
 __device__ void cold_replay(const TraceArgs &a, const SplitArgs &sp, int i, double x[3], double N[3], int k) {
     const TileCell cg{a.cellp, nullptr, 0, 0, 0, 0};
     const TileCoef ng{a.coef, nullptr, 0, 0, 0, 0};
+    ZBox zb;  // (unused: the replay stores no zero flags)
     for (int s = 0; s < k; s++) {
         double xn[3], Nn[3], psi;
         if (sp.traj_mode == kTrajCell)
-            cold_step<true, kTileNS, TileCell, true>(a, cg, sp, 0, i, x, N, xn, Nn, &psi);
+            cold_step<true, kTileNS, TileCell, true>(a, cg, sp, 0, i, x, N, xn, Nn, &psi, zb, false);
         else if (sp.traj_mode == kTrajTile)
-            cold_step<true, kTileNS, TileCoef, true>(a, ng, sp, 0, i, x, N, xn, Nn, &psi);
+            cold_step<true, kTileNS, TileCoef, true>(a, ng, sp, 0, i, x, N, xn, Nn, &psi, zb, false);
         else
-            cold_step<true, kNF, const double *, true>(a, a.coef, sp, 0, i, x, N, xn, Nn, &psi);
+            cold_step<true, kNF, const double *, true>(a, a.coef, sp, 0, i, x, N, xn, Nn, &psi, zb, false);
 #pragma unroll
         for (int c = 0; c < 3; c++) {
             x[c] = xn[c];
@@ -3105,6 +3171,11 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
                  b_awork = a.counters ? al(4 * sizeof(unsigned) * n * kb) : 0,
                  b_psib = DM == kDepoBinned ? al(sizeof(double) * n * kb) : 0,
                  b_cbx = al(6 * sizeof(double) * n * n_cb), b_n8 = al(8 * n), b_n4 = al(4 * n);
+    // the block zero flags (ZBox): Albajar with the early settle on (GLTable::negl_skip);
+    // TORJ_ALPHA_ZFLAG=0 (read per call) turns them off
+    const char *zf_e = getenv("TORJ_ALPHA_ZFLAG");
+    const bool zflag_on = a.abs_model == 1 && g_gl_host.negl_skip && !(zf_e && atoi(zf_e) == 0);
+    const size_t b_zf = zflag_on ? al(n) : 0;
     // the streamed deposition's per-ray walk state (fa: the reference profile;
     // TORJ_DEPO_STREAM=0 runs the whole walk after the trace instead)
     // TORJ_DEPO_STREAM=1: the windows on the scan's stream, after each scan;
@@ -3132,7 +3203,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     const size_t b_defer = a.abs_model >= 2 ? al(4 * sizeof(unsigned long long) * n * kb) : 0,
                  b_dcnt = a.abs_model >= 2 ? al(sizeof(unsigned) * n_blk) : 0;
     const size_t bytes = R * (b_ain + b_alpha + b_awork) + R * b_psib + b_cbx + 6 * b_n8 + 3 * b_n8 +
-                         2 * b_n4 + b_dsd + b_dsi + b_defer + b_dcnt;
+                         2 * b_n4 + b_dsd + b_dsi + b_defer + b_dcnt + R * b_zf;
     if (ensure_split(p, bytes)) return -1;
     char *q = (char *)p->d_split;
     auto take = [&](size_t b) {
@@ -3153,6 +3224,9 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
     double *psib[R] = {};
     if (b_psib)
         for (int r = 0; r < R; r++) psib[r] = (double *)take(b_psib);
+    unsigned char *zflags[R] = {};
+    if (b_zf)
+        for (int r = 0; r < R; r++) zflags[r] = (unsigned char *)take(b_zf);
     sp.cbx = (double *)take(b_cbx);
     sp.tx = (double *)take(6 * b_n8);
     sp.stau = (double *)take(b_n8);
@@ -3269,6 +3343,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         const int r = b % R;
         sp.ain = ain[r];
         sp.psib = psib[r];
+        sp.zflag = zflags[r];
         sp.alpha = alphas[r];
         sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done

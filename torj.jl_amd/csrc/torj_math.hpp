@@ -1185,7 +1185,7 @@ TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, doub
 // profiling build only (tools/alpha_prof.py): [2 (m - 2)] waves and [2 (m - 2) + 1]
 // lanes that ran harmonic m's node loop, [4] waves and [5] live lanes of k_alpha_pts;
 // [6 ..] waves that reached a region of abs_albajar_fast_body (kAprof*)
-enum { kAprofTe = 6, kAprofPro, kAprofOk, kAprofH2, kAprofB2, kAprofH3, kAprofB3, kAprofN = 13 };
+enum { kAprofTe = 6, kAprofPro, kAprofOk, kAprofH2, kAprofB2, kAprofH3, kAprofB3, kAprofZ, kAprofN = 14 };
 #ifdef TORJ_TRAJ_TU
 static
 #endif
