@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 O=gpurun_out/${OUT:-call}
 mkdir -p $O
 if [ -n "$PYTEST_K" ] || [ -n "$PYTEST_FILES" ]; then
-  timeout -k 10 ${PYTEST_T:-700} python -u -m pytest ${PYTEST_FILES:-tests} -x -v -m gpu ${PYTEST_K:+-k "$PYTEST_K"} \
+  timeout -k 10 ${PYTEST_T:-700} python -u -m pytest ${PYTEST_FILES:-tests} -x -v ${PYTEST_S:+-s} -m gpu ${PYTEST_K:+-k "$PYTEST_K"} \
       --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
   rc=$?
   tail -4 $O/pytest.log

@@ -92,8 +92,8 @@ def test_split_counters_match_fused(gpu, T, hplasma, zflag):
     equal the fused kernel's on a beam without mid-block stops.  With the block
     zero flags (TORJ_ALPHA_ZFLAG, the default) a wave whose rays are all flagged
     evaluates nothing, so its points count no settled-early harmonics (counter
-    7): that counter is then at most the fused kernel's, the others equal, and
-    the outputs the same bits."""
+    7): that counter is then at most the fused kernel's and the others equal
+    (the outputs' bits: test_zero_flags_bit_identical)."""
     import ctypes
     import torch
 
@@ -133,6 +133,61 @@ def test_split_counters_match_fused(gpu, T, hplasma, zflag):
     else:
         assert np.array_equal(cf[:7], cs[:7]) and cs[7] <= cf[7], (cf, cs)
         print(f"settled-early harmonics counted: fused {cf[7]}, split with zero flags {cs[7]}")
+
+
+@pytest.mark.parametrize("tiny", ["1e-20", "0"])
+def test_zero_flags_bit_identical(gpu, T, hplasma, tiny):
+    """The block zero flags (torj_hip.hip zero_box_flag: the trajectory kernel
+    proves per ray and ring block that every stored stage point has alpha = +-0,
+    and an alpha wave whose rays are all flagged writes 0 without evaluating)
+    change no output bit: TORJ_ALPHA_ZFLAG=0 against the default on the split
+    path, with the tiny-alpha skip (default) and without it (the exact leg), on
+    a fan whose rays start outside the resonance (flagged blocks) and cross it
+    (unflagged ones), with mid-trace stops; statuses, steps, state, trajectory
+    samples, P_dep and dP_shell all equal."""
+    pos, xp, Np, s0, w, om = _fan(T, hplasma)
+    kw = dict(ds=1e-4, n_steps=3000, chunk_steps=30, weights=w, traj_stride=30, P_min=5e-2,
+              psi_grid=np.linspace(0, 1, 500), deposition="reference", x_launch=pos, s0=s0)
+    out, cnts = {}, {}
+    old = {k: os.environ.get(k) for k in ("TORJ_ALPHA_ZFLAG", "TORJ_TINY_ALPHA")}
+    os.environ["TORJ_TINY_ALPHA"] = tiny
+    T.abs_Al_init(24)
+    try:
+        for z in ("0", "1"):
+            os.environ["TORJ_ALPHA_ZFLAG"] = z
+            out[z] = _run(T, hplasma, 3, 60, xp, Np, om, 1, **kw)
+            cnts[z] = _trace_counted(T, hplasma, 3, xp, Np, om)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        T.abs_Al_init(24)
+    a, b = out["0"], out["1"]
+    assert a.status.tolist().count(T.ABSORBED) >= 10, "need mid-trace stops"
+    for f in ("state", "status", "steps", "P_dep", "dP_shell"):
+        assert np.array_equal(getattr(a, f), getattr(b, f)), f
+    assert np.array_equal(a.traj, b.traj, equal_nan=True)
+    c0, c1 = cnts["0"], cnts["1"]
+    assert np.array_equal(c0[:7], c1[:7]) and c1[7] <= c0[7], (c0, c1)
+    print(f"tiny_alpha {tiny}: counters without flags {c0}, with {c1}")
+    if tiny != "1e-20":
+        return
+    # the flags fire: under the test hook TORJ_TEST_ZFLAG_NAN=s a fully flagged
+    # wave of a block starting at step s or later writes NaN, so its live rays
+    # stop NAN at the first step of that block (a multiple of the 60-step block);
+    # every other ray is untouched
+    for s_from in (0, 60):
+        h = _env_run(T, hplasma, {"TORJ_TEST_ZFLAG_NAN": str(s_from)}, xp, Np, om, 1, **kw)
+        nan = h.status == T.NAN
+        print(f"from step {s_from}: flagged waves stop {nan.sum()} of {len(nan)} rays, at steps "
+              f"{np.unique(h.steps[nan], return_counts=True)}")
+        assert nan.sum() >= 64
+        assert (h.steps[nan] % 60 == 0).all() and (h.steps[nan] >= s_from).all()
+        assert (h.steps[nan] < a.steps[nan]).all()
+        for f in ("state", "status", "steps"):
+            assert np.array_equal(getattr(h, f)[~nan], getattr(b, f)[~nan]), f
 
 
 def test_split_on_129_grid_vs_oracle(gpu, T, O):

@@ -917,6 +917,8 @@ struct SplitArgs {
     int *sinfo;           // steps | status << 24: the scan's stop
     unsigned char *zflag;  // per ray, this block (ring slot): 1 = Albajar alpha provably +-0 at every
                            // stage point the trajectory kernel stored (zero_box_flag); null: off
+    double zval;           // what a fully flagged alpha wave writes: 0, or NaN under the test hook
+                           // TORJ_TEST_ZFLAG_NAN=1 (the flagged waves then stop their rays NAN)
     int k0, kb;           // block: steps [k0, k0 + kb)
     int nf;               // alpha input fields per point: kAinF (Albajar) or kAinFW (warm)
     int tile_cap;         // k_traj_tile: most nodes a wave stages (<= kTileNodes)
@@ -1410,7 +1412,7 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
 #if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
         TORJ_APROF_WAVE(kAprofZ);
 #endif
-        sp.alpha[(size_t)js * a.n + i] = 0.0;
+        sp.alpha[(size_t)js * a.n + i] = sp.zval;
         if constexpr (COUNT) sp.awork[(size_t)js * a.n + i] = 0u;
         return;
     }
@@ -3316,6 +3318,18 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
             fprintf(stderr, "libtorj_hip: TORJ_TEST_NAN_ALPHA_STEP=%d is set -- a TEST HOOK: alpha is "
                             "read as NaN at that step for every third ray\n", sp.nan_step);
     }
+    // test hook only (tests/test_gpu_split.py): TORJ_TEST_ZFLAG_NAN=s -- the fully
+    // flagged alpha waves of the blocks that start at step s or later write NaN
+    // instead of 0, so that the rays they hold stop NAN where the flags fired
+    const char *zn_e = getenv("TORJ_TEST_ZFLAG_NAN");
+    const int zflag_nan_from = zn_e ? std::max(0, atoi(zn_e)) : -1;
+    sp.zval = 0.0;
+    if (zflag_nan_from >= 0) {
+        static std::atomic<bool> warned{false};
+        if (!warned.exchange(true))
+            fprintf(stderr, "libtorj_hip: TORJ_TEST_ZFLAG_NAN is set -- a TEST HOOK: fully flagged alpha "
+                            "waves write NaN\n");
+    }
     const char *dl_e = getenv("TORJ_WARM_DEFER_LRM");
     sp.defer_lrm = dl_e ? std::min(3, std::max(0, atoi(dl_e))) : 3;
     const size_t lds_bytes = (size_t)(a.g.nR + 2) * (a.g.nZ + 2) * kTrajLdsNS * sizeof(double);
@@ -3344,6 +3358,7 @@ static int split_trace(torj_plasma_s *p, TraceArgs a, int DM, bool tr, int cs, h
         sp.ain = ain[r];
         sp.psib = psib[r];
         sp.zflag = zflags[r];
+        sp.zval = (zflag_nan_from >= 0 && sp.k0 >= zflag_nan_from) ? NAN : 0.0;
         sp.alpha = alphas[r];
         sp.awork = b_awork ? aworks[r] : nullptr;  // work words only for a counted launch
         // this ring slot's previous readers (alpha and scan of block b - R) are done
