@@ -1012,6 +1012,27 @@ def _parity(OP, r, idx, xp, Np, omega, args, gpu_out, threads):
                       f"relative, i.e. {1e-6 * {1: 1e-10, 2: 1e-8, 3: 1e-9}.get(model, 1e-10):g} "
                       f"absolute below tau = 1e-6 (the floor: P moves by < 1 ulp there); status "
                       f"and steps exact")}
+    if model == 1 and resolv.any():
+        # the resolvable rays outside the bar unfloored: the oracle's a-priori
+        # sensitivity (or_albajar_sensitivity, from the trajectory alone: tau's change
+        # when every stage point's alpha inputs move by 2^-45 relative) for each;
+        # flagged beyond half the bar, as the C5 line flags (tools/c3_tau_diag.py
+        # runs it on every resolvable ray: DESIGN.md 3.7)
+        out = np.nonzero(resolv & (et_strict > parity["bar_rel"]))[0]
+        sens = (OP.albajar_sensitivity(xp[idx[out]], Np[idx[out]], omega, args.mode, args.ds,
+                                       r["steps"][out], n_threads=threads) if len(out) else np.zeros(0))
+        fl = ~(sens <= 0.5 * parity["bar_rel"] * np.abs(os_[out, 6]))
+        keep = resolv.copy()
+        keep[out[fl]] = False
+        parity["tau_resolvable_conditioning"] = {
+            "rays_out_of_bar": int(len(out)), "rays_out_of_bar_flagged": int(fl.sum()),
+            "max_rel_tau_resolvable_excl_flagged": float(et_strict[keep].max()) if keep.any() else None,
+            "out_of_bar": [{"fan_index": int(idx[k]), "tau_cpu": float(os_[k, 6]), "rel": float(et_strict[k]),
+                            "sens_over_tau": float(sv / abs(os_[k, 6])), "flagged": bool(f)}
+                           for k, sv, f in zip(out[:16], sens[:16], fl[:16])],
+            "flag": "oracle or_albajar_sensitivity over the ray's stage points with inputs moved by "
+                    "2^-45 relative exceeds half the bar: tau not determined to 1e-10 by a double-"
+                    "precision restatement (a harmonic's threshold, alpha ~ sqrt(r^2 - 1))"}
     if warm:
         # a-priori conditioning flag: how far each sampled ray's tau
         # moves when every RK4 stage point's warm-alpha inputs move by 2^-45 relative

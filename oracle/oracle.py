@@ -239,6 +239,19 @@ class OraclePlasma:
                                   C.c_double(eta), _p(out), n_threads or default_threads())
         return out
 
+    def albajar_sensitivity(self, x0, N0, omega, mode, ds, steps, eta=2.0 ** -45, n_threads=None):
+        """or_albajar_sensitivity: warm_sensitivity's a-priori flag for the Albajar
+        model -- per ray, the sum over its RK4 stage points of ds w_stage max |d alpha|
+        under relative perturbations eta of Y, and of (X, N_par, Te) jointly."""
+        x0, N0 = _c(x0).reshape(-1, 3), _c(N0).reshape(-1, 3)
+        n = x0.shape[0]
+        st = np.ascontiguousarray(steps, dtype=np.int32)
+        out = np.zeros(n)
+        lib().or_albajar_sensitivity(self.ref, C.c_double(omega), C.c_int(mode), C.c_double(ds), n,
+                                     _p(x0), _p(N0), st.ctypes.data_as(_ip), C.c_double(eta),
+                                     _p(out), n_threads or default_threads())
+        return out
+
     def alpha_approx(self, x, N, omega, mode):
         return lib().or_alpha_approx(self.ref, _p(_c(x)), _p(_c(N)), C.c_double(omega),
                                      C.c_int(mode))

@@ -1239,6 +1239,65 @@ void or_warm_sensitivity(const or_plasma *p, double omega, int mode, int iwarm, 
     }
 }
 
+/* The same a-priori sensitivity for the Albajar model (absorption 1, the C3
+ * parity statistic over resolvable optical depths): each stage point's
+ * abs_Albajar_fast re-evaluated with Y moved up and down by eta, and with
+ * (X, N_par, Te) jointly both ways.  Near a harmonic's threshold (r = m / m_0
+ * just above 1) alpha carries sqrt(r^2 - 1), whose relative change under a
+ * relative change eta of Y is eta r^2 / (r^2 - 1): a ray whose tiny optical
+ * depth comes from such points has a tau that inputs differing by a few ulps
+ * (the GPU's trajectory against this one's, 1e-15) move beyond 1e-10. */
+static double albajar_stage_sens(const or_plasma *p, const double u[6], double omega, int mode,
+                                 double eta) {
+    double X, Y, Npar, b[3];
+    or_eval_plasma(p, u, u + 3, omega, &X, &Y, &Npar, b);
+    const double Nabs = sqrt(u[3] * u[3] + u[4] * u[4] + u[5] * u[5]);
+    const double Te = or_T_e(p, u);
+    const double a0 = or_abs_albajar_fast(omega, X, Y, Nabs, Npar, Te, mode);
+    static const double f[4][4] = {{0, 1, 0, 0}, {0, -1, 0, 0}, {1, 0, 1, -1}, {-1, 0, -1, 1}};
+    double d = 0.0;
+    for (int k = 0; k < 4; k++) {
+        const double a = or_abs_albajar_fast(omega, X * (1.0 + eta * f[k][0]), Y * (1.0 + eta * f[k][1]),
+                                             Nabs, Npar * (1.0 + eta * f[k][2]),
+                                             Te * (1.0 + eta * f[k][3]), mode);
+        const double e = fabs(a - a0);
+        if (!(e <= d)) d = e;
+    }
+    return d;
+}
+
+void or_albajar_sensitivity(const or_plasma *p, double omega, int mode, double ds, int n_rays,
+                            const double *x0, const double *N0, const int *steps, double eta,
+                            double *out_sens, int n_threads) {
+    int nth = n_threads > 0 ? n_threads : 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nth)
+#endif
+    for (int r = 0; r < n_rays; r++) {
+        double u[6], sens = 0.0;
+        for (int k = 0; k < 3; k++) {
+            u[k] = x0[3 * r + k];
+            u[3 + k] = N0[3 * r + k];
+        }
+        for (int s = 0; s < steps[r]; s++) {
+            double k1[6], k2[6], k3[6], k4[6], ut[6], dummy;
+            rhs(p, u, omega, mode, 0, k1, &dummy);
+            sens += ds / 6.0 * albajar_stage_sens(p, u, omega, mode, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + 0.5 * ds * k1[k];
+            rhs(p, ut, omega, mode, 0, k2, &dummy);
+            sens += ds / 3.0 * albajar_stage_sens(p, ut, omega, mode, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + 0.5 * ds * k2[k];
+            rhs(p, ut, omega, mode, 0, k3, &dummy);
+            sens += ds / 3.0 * albajar_stage_sens(p, ut, omega, mode, eta);
+            for (int k = 0; k < 6; k++) ut[k] = u[k] + ds * k3[k];
+            rhs(p, ut, omega, mode, 0, k4, &dummy);
+            sens += ds / 6.0 * albajar_stage_sens(p, ut, omega, mode, eta);
+            for (int k = 0; k < 6; k++) u[k] = u[k] + ds / 6.0 * (k1[k] + 2.0 * k2[k] + 2.0 * k3[k] + k4[k]);
+        }
+        out_sens[r] = sens;
+    }
+}
+
 /* shell index j with grid[j] <= v < grid[j+1]; clamps to [0, n-2] */
 static int shell_of(const double *g, int n, double v) {
     int lo = 0, hi = n - 1;

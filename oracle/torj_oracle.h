@@ -177,6 +177,10 @@ int or_trace(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const doub
 void or_warm_sensitivity(const or_plasma *p, double omega, int mode, int iwarm, double ds,
                          int n_rays, const double *x0, const double *N0, const int *steps,
                          double eta, double *out_sens, int n_threads);
+/* the same for the Albajar model (abs_Albajar_fast's inputs X, Y, N_par, Te) */
+void or_albajar_sensitivity(const or_plasma *p, double omega, int mode, double ds, int n_rays,
+                            const double *x0, const double *N0, const int *steps, double eta,
+                            double *out_sens, int n_threads);
 int or_trace_samples(const or_plasma *p, const or_trace_cfg *cfg, int n_rays, const double *x0,
                      const double *N0, const double *weights, double *out_state, int *out_status,
                      int *out_steps, double *out_dP, double *out_Pdep, double *out_traj,

@@ -125,3 +125,27 @@ def test_tiny_alpha_and_resolvable_tau_statistic(monkeypatch):
     assert abs(p["max_rel_tau_resolvable"] - 4e-11) < 1e-15
     assert p["max_rel_tau_unfloored"] == 1.0
     assert p["rays_within_bar"] == n  # the floored bar holds for all four
+    c = p["tau_resolvable_conditioning"]
+    assert c["rays_out_of_bar"] == 0 and c["max_rel_tau_resolvable_excl_flagged"] == p["max_rel_tau_resolvable"]
+
+    # a resolvable ray outside the bar unfloored: the oracle's a-priori
+    # sensitivity decides whether it is flagged (beyond half the bar) and left
+    # out of the excl_flagged statistic
+    class OP:
+        def __init__(self, sens):
+            self.sens = sens
+
+        def albajar_sensitivity(self, x0, N0, omega, mode, ds, steps, n_threads=None):
+            assert len(x0) == len(steps) == 1
+            return np.array([self.sens])
+
+    gpu[2, 6] = st[2, 6] * (1 + 6e-10)
+    xp = np.zeros((n, 3))
+    for sens, flagged in ((1e-19, True), (1e-23, False)):
+        p = B._parity(OP(sens), r, np.arange(n), xp, xp, 0.0, Args,
+                      (gpu, np.zeros(n, np.int32), np.full(n, 2000, np.int32)), 1)
+        c = p["tau_resolvable_conditioning"]
+        assert c["rays_out_of_bar"] == 1 and c["rays_out_of_bar_flagged"] == int(flagged)
+        assert c["out_of_bar"][0]["fan_index"] == 2
+        want = 1e-12 if flagged else 6e-10
+        assert abs(c["max_rel_tau_resolvable_excl_flagged"] - want) < 0.1 * want

@@ -198,3 +198,22 @@ def test_c5_conditioning_flag_and_the_50_digit_evidence(O, oplasma):
     mp = float(warm_mp.alpha_warm_wr(*p, 1))
     prev = float(warm_mp.alpha_warm_wr(*pts[135], 1))
     assert abs(mp - 0.7739104) < 1e-6 and abs(prev - mp) < 1e-4 * mp
+
+
+def test_c3_tau_conditioning_flag(oplasma):
+    """The C3 line's conditioning statistic (bench.py tau_resolvable_conditioning,
+    oracle or_albajar_sensitivity): fan ray 88266 -- tau 1.79e-12, the one sampled
+    ray with tau_cpu >= 1e-12 outside 1e-10 unfloored in round 6 (5.8e-10; the
+    fused kernel 4e-11) -- moves by ~8e-8 of its tau when its stage points'
+    Albajar inputs move by 2^-45 relative, so it is flagged; a ray of ordinary
+    tau (20731) is not.  The sensitivity is linear in the perturbation."""
+    idx = np.array([88266, 20731])
+    xp, Np, om = _c5_rays(idx)
+    r = oplasma.trace(xp, Np, om, 1, 1e-4, 2000, absorption=1)
+    tau = r["state"][:, 6]
+    assert 1e-12 < tau[0] < 3e-12 and tau[1] > 1e-6, tau
+    sens = oplasma.albajar_sensitivity(xp, Np, om, 1, 1e-4, r["steps"])
+    rel = sens / tau
+    assert rel[0] > 1e-8 and rel[1] < 0.5e-10, rel
+    half = oplasma.albajar_sensitivity(xp, Np, om, 1, 1e-4, r["steps"], eta=2.0 ** -46)
+    assert np.all(np.abs(half / sens - 0.5) < 0.1), half / sens
