@@ -52,11 +52,9 @@ def main():
              "h3_not_zero", "h3_bound", "zero_flag_waves"]
     out["region_waves"] = {nm: v[6 + k] for k, nm in enumerate(names)}
     out["region_waves_per_kernel_wave"] = {nm: v[6 + k] / max(v[4], 1) for k, nm in enumerate(names)}
-    # harmonic-2 node pairs (n = 24: 12 per node loop) that a rigorous per-pair
-    # bound proves below 2^-62 of the running sum (wave-uniform), and of the final sum
-    pairs = 12 * v[0]
-    out["h2_pairs"] = {"pairs": pairs, "skippable_running": v[14], "skippable_final": v[15],
-                       "frac_running": v[14] / max(pairs, 1), "frac_final": v[15] / max(pairs, 1)}
+    # live lanes of the evaluated (not fully flagged) waves that carry a zero flag
+    out["flagged_lanes_in_evaluated_waves"] = v[14]
+    out["flagged_lane_fraction_of_evaluated"] = v[14] / max(v[5], 1)
     print(json.dumps(out, indent=1))
 
 

@@ -1422,10 +1422,13 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     if (sp.k0 + j >= info_steps(ti) || info_status(si) != ST_OK) return;
 #if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
     {
-        const unsigned long long am = __ballot(1);
+        // [14]: the live lanes of these (not fully flagged) waves that carry a
+        // zero flag -- what compacting the unflagged points into full waves would save
+        const unsigned long long am = __ballot(1), zm = __ballot(zf != 0);
         if ((int)__lane_id() == __builtin_ffsll((long long)am) - 1) {
             atomicAdd(&g_aprof[4], 1ull);
             atomicAdd(&g_aprof[5], (unsigned long long)__popcll(am));
+            atomicAdd(&g_aprof[14], (unsigned long long)__popcll(zm));
         }
     }
 #endif

@@ -1009,18 +1009,6 @@ struct HarmConst {
     double hx2, K1h, K5h;  // hx^2, K1 / hx = 2 Axz ea / m, K5 / hx = 2 q ea e3 / m (pair_term)
 };
 
-// 2 (P'max + Q'max): with |S_nu| <= 1 / nu! (|J_nu(x)| <= (x/2)^nu / nu!),
-// |u| <= hx^2 / (m+1)!, |D| <= 1/(m-1)! + hx^2 / (m+1)!, a bound on pair_term's
-// |P' (E+ + E-) + t Q' (E+ - E-)| / max(E+, E-) (pair_term's notation)
-template <int M>
-TORJ_HD double pair_bound_const(const HarmConst &c) {
-    constexpr double iS = inv_fact(M), iS1 = inv_fact(M + 1), iSl = inv_fact(M - 1);
-    const double um = c.hx2 * iS1, Dm = iSl + um;
-    const double Pm = iS * iS * (fabs(c.K0) + fabs(c.K3)) + fabs(c.K2) * iSl * um + fabs(c.K1h) * iS * Dm;
-    const double Qm = fabs(c.K4) * iS * iS + fabs(c.K5h) * iS * Dm;
-    return 2.0 * (Pm + Qm);
-}
-
 // A symmetric pair of Gauss-Legendre nodes (+t, -t): w * pol_fact * exp(mu (1 -
 // gamma)) summed over both, without the node-independent factor (-mu) (m / (N_perp
 // omega_bar))^2.  GL nodes are symmetric with equal weights, and the Bessel
@@ -1152,47 +1140,17 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
     // consumed at the end of the iteration, is scheduled late by the compiler
     // anyway, and the other waves of the SIMD cover the latency)
     int i = 0;
-#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    // profiling build only: how many of the wave's node pairs a rigorous
-    // per-pair bound (pair_bound_const x the pair's largest exponential) proves
-    // below 2^-62 of the running sum (skippable bit-exactly, [14]) or of the final
-    // sum ([15]: what a dominant-first order could skip)
-    const double pqb = pair_bound_const<M>(c);
-    double pb[kMaxGL / 2];
-    int nrun = 0;
-#endif
 #pragma unroll 1
     for (; i + U <= half; i += U) {
         double r[U];
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const GLTable::Node q = nd[i + u];
-#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
-            if (U == 1 && LPR == 1) {
-                const double a = fma(c.C1, q.t2, c.C0), b = c.C2 * q.t;
-                const double y = c.mu2 * (1.0 - sqrt(a - fabs(b)));
-                const double B = q.wm * pqb * exp2(fmin(y, 1000.0) + 1.0);
-                pb[i] = B;
-                if (__all(B < 0x1p-62 * fabs(acc[0]))) nrun++;
-            }
-#endif
             r[u] = pair_term<M, LV>(c, sc, q.t, q.s2, q.wm, q.t2, false);
         }
 #pragma unroll
         for (int u = 0; u < U; u++) acc[u] += r[u];
     }
-#if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
-    if (U == 1 && LPR == 1) {
-        int nfin = 0;
-        for (int k = 0; k < half && k < kMaxGL / 2; k++)
-            if (__all(pb[k] < 0x1p-62 * fabs(acc[0]))) nfin++;
-        const unsigned long long am = __ballot(1);
-        if ((int)__lane_id() == __builtin_ffsll((long long)am) - 1) {
-            atomicAdd(&g_aprof[14], (unsigned long long)nrun);
-            atomicAdd(&g_aprof[15], (unsigned long long)nfin);
-        }
-    }
-#endif
     // the remainder pairs (none when U = 1: the compiler still materialised the
     // pair's constants for this loop's preheader, ~67 SALU per node loop)
     if constexpr (U > 1) {
