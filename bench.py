@@ -632,6 +632,8 @@ def main_library(args):
                             f"ray shards, RCCL all-reduce of dP_shell"),
             "placement": placement,
             "n_devices_used": len(devs),
+            "tiny_alpha": tiny_alpha(),
+            "build_id": L.torj_build_id().decode(),
         },
         "roofline": {
             "bound": "fp64-valu",
