@@ -47,10 +47,11 @@ SPLIT_KERNELS = "k_traj|k_alpha_pts|k_tau_scan|k_split_final"
 # version of the FLOP model behind roofline.achieved (torj_hip/flops.py); bumped
 # whenever a counter's meaning or a per-unit price changes, so figures of
 # different rounds are compared only under the same model
-FLOP_MODEL = {"albajar": "albajar-v4 (round 5: harmonics skipped below tiny_alpha = 1e-20 m^-1 priced as "
+FLOP_MODEL = {"albajar": "albajar-v5 (round 6: the node loop's gamma as the resonance condition's linear "
+                         "form G0 +- G1 t, no square root; round 5: harmonics skipped below tiny_alpha = 1e-20 m^-1 priced as "
                          "negligible ones; round 3: exact-zero, negligible and settled-early harmonics "
                          "priced at their tests)",
-              "none": "albajar-v4",
+              "none": "albajar-v5",
               "warm_wr": "warm-v3 (round 5: warmdisp's breaking pass sums no tensor, its root by "
                          "the conjugate product, the asymptotic Faddeeva series by Horner; round 3: counter[2] = asymptotic Faddeeva "
                          "evaluations; larmornumber tests priced at one per call, a lower bound)"}

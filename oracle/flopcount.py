@@ -227,7 +227,8 @@ def series_coef(nu, k, x_m):
 def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m, count=None):
     """Node-pair form of abs_Al_integral_nume_fast x sqrt((m/m0)^2-1) (torj_math.hpp
     albajar_harmonic + pair_term, TORJ_PAIR_V2): the pair (+t, -t) shares every
-    t-even factor, bracket(+-t) = P +- t Q, gamma(+-t)^2 = C0 + C1 t^2 +- C2 t."""
+    t-even factor, bracket(+-t) = P +- t Q, and gamma(+-t) = G0 +- G1 t, the
+    resonance condition's linear form (harm_geom, TORJ_NODE_GAMMA_LIN, round 6)."""
     md = float(m)
     inv_md = 1.0 / md  # compile-time constant
     r2m1 = r * r - 1.0
@@ -240,10 +241,10 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m
     K3 = q * q * e3 * e3
     K4 = 2.0 * q * Axz * e3
     K5 = q * ea * e3 * x_m * inv_md
-    upa0, upa1 = inv_sqNp * r * Npar, inv_sqNp * sq_r
-    C0 = upa0 * upa0 + r * r
-    C1 = r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp)
-    C2 = 2.0 * upa0 * upa1
+    upa1 = inv_sqNp * sq_r
+    # node exponent mu (1 - gamma(+-t)) = Y0 -+ Y1 t (the device takes it in base 2)
+    Y0 = mu - mu * (r * inv_sqNp)
+    Y1 = mu * (Npar * upa1)
     hx = 0.5 * x_m
     K = series_terms(x_m.v)
     if count is not None:
@@ -274,20 +275,18 @@ def albajar_harmonic(gl, mu, r, Npar, inv_sqNp, Nperp, omega_bar, Axz, ea, e3, m
         Cc = st * Sm * (Sl - T1)
         P = A * (K3 * t2 + K0) + (Cc * K1 - B)
         wp = w * p
-        a = C1 * t2 + C0
         n_node = 0
         if single:
             n1 = Counter.n
-            E = exp(mu - mu * sqrt(a))
+            E = exp(Y0)
             n_node = Counter.n - n1
             total = total + wp * P * E
         else:
             Q = A * K4 + Cc * K5
-            b = C2 * t
             n1 = Counter.n
-            Ep = exp(mu - mu * sqrt(a + b))
+            Ep = exp(Y0 - Y1 * t)
             n_node = Counter.n - n1
-            Em = exp(mu - mu * sqrt(a - b))
+            Em = exp(Y0 + Y1 * t)
             total = total + wp * (P * (Ep + Em) + (t * Q) * (Ep - Em))
         if count is not None and "node" not in count:
             count["node"] = n_node

@@ -1006,6 +1006,7 @@ struct HarmConst {
     double mu2;  // mu log2(e): the node exponent in base 2 (exp2_node)
     // node-pair form: gamma_pm^2 = C0 + C1 t^2 pm C2 t, h = hx sqrt(1-t^2)
     double C0, C1, C2, hx;
+    double Y0, Y1;  // node exponents mu log2(e) (1 - gamma(+-t)) = Y0 -+ Y1 t (TORJ_NODE_GAMMA_LIN)
     double hx2, K1h, K5h;  // hx^2, K1 / hx = 2 Axz ea / m, K5 / hx = 2 q ea e3 / m (pair_term)
 };
 
@@ -1018,6 +1019,10 @@ struct HarmConst {
 // middle node of an odd-order rule, t = 0).
 #ifndef TORJ_PAIR_UNROLL
 #define TORJ_PAIR_UNROLL 1
+#endif
+#ifndef TORJ_NODE_GAMMA_LIN  // the node loop's gamma as the resonance condition's linear form
+// G0 +- G1 t (1, round 6) or as the reference's sqrt(1 + u_par^2 + u_perp^2) (0; harm_geom)
+#define TORJ_NODE_GAMMA_LIN 1
 #endif
 
 // Series coefficients of one harmonic for the node loop (compile-time
@@ -1085,12 +1090,21 @@ TORJ_HD double pair_term(const HarmConst &c, const SeriesCoefs<M, LV> &sc, doubl
     const double D = Sl - u;
     const double Sm2 = Sm * Sm, SmD = Sm * D;
     const double P = fma(Sm2, fma(c.K3, t2, c.K0), fma(c.K1h, SmD, -(c.K2 * (Sl * u))));
+#if TORJ_NODE_GAMMA_LIN
+    // gamma(+-t) = G0 +- G1 t on the resonance ellipse (harm_geom): the node
+    // exponents are two fma, no square root
+    if (single) return W * (P * exp2_node(c.Y0));
+    const double Q = fma(c.K4, Sm2, c.K5h * SmD);
+    const double Ep = exp2_node(fma(-c.Y1, t, c.Y0));
+    const double Em = exp2_node(fma(c.Y1, t, c.Y0));
+#else
     const double a = fma(c.C1, t2, c.C0);
     if (single) return W * (P * exp2_node(fma(-c.mu2, sqrt_node(a), c.mu2)));
     const double Q = fma(c.K4, Sm2, c.K5h * SmD);
     const double b = c.C2 * t;
     const double Ep = exp2_node(fma(-c.mu2, sqrt_node(a + b), c.mu2));
     const double Em = exp2_node(fma(-c.mu2, sqrt_node(a - b), c.mu2));
+#endif
     return W * fma(P, Ep + Em, (t * Q) * (Ep - Em));
 }
 
@@ -1171,6 +1185,7 @@ TORJ_HD double node_sum(const GLTable &gl, const HarmConst &c, int sub = 0) {
 // before the polarisation vector and can settle alpha = 0 there.
 struct HarmGeom {
     double r, r2m1, sq_r, upa0, upa1, C0, C1, C2, qmin;
+    double Y0, Y1, ymax;  // TORJ_NODE_GAMMA_LIN: node exponents Y0 -+ Y1 t, their bound
     bool zero;
 };
 
@@ -1181,6 +1196,30 @@ TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, doub
     g.sq_r = sqrt_nn(g.r2m1);
     g.upa0 = inv_sqNp * r * Npar;
     g.upa1 = inv_sqNp * g.sq_r;
+#if TORJ_NODE_GAMMA_LIN
+    // The ellipse is the square of the resonance condition gamma = m Y + N_par u_par
+    // (src/absorption.jl:176-179 parametrise it by u_par = upa0 + upa1 t and
+    // u_perp^2 = (r^2 - 1)(1 - t^2)), and with m Y = r sqrt(1 - N_par^2) that is
+    //   gamma(t) = G0 + G1 t,  G0 = r / sqrt(1 - N_par^2),  G1 = N_par upa1,
+    // positive over the whole ellipse (|N_par| < 1 and sqrt(r^2 - 1) < r): the
+    // value of the reference's sqrt(1 + u_par^2 + u_perp^2) without the square
+    // root, both forms within a few ulp of the exact gamma.  In base 2 the node
+    // exponent mu log2(e) (1 - gamma(+-t)) is Y0 -+ Y1 t; its largest value over
+    // |t| <= 1 is ymax = Y0 + |Y1| (gamma_min = G0 - |G1|: gamma is monotone in t).
+    const double mu2 = mu * 1.4426950408889634074;
+    g.Y0 = fma(-mu2, r * inv_sqNp, mu2);
+    g.Y1 = mu2 * (Npar * g.upa1);
+    g.ymax = g.Y0 + fabs(g.Y1);
+    // Exact zero: every node's 2^y underflows to +0 (exp2_node returns exactly 0
+    // below y = -1076) when ymax < -1096 -- round 3's mu (gamma_min - 1) > 760 in
+    // base 2, whose margin covers the roundings of ymax and of each node's y (a
+    // few 1e-13).  Then the node sum is +-0 and the loop is skipped with the same
+    // value; NaN operands never skip.
+    g.zero = g.ymax < -1096.0;
+    g.C0 = g.C1 = g.C2 = g.qmin = 0.0;  // (the square-root form's, unused)
+    (void)inv_mu;
+#else
+    g.Y0 = g.Y1 = g.ymax = 0.0;
     g.C0 = fma(g.upa0, g.upa0, r * r);
     g.C1 = g.r2m1 * (Npar * Npar) * (inv_sqNp * inv_sqNp);  // u_par1^2 - (r^2 - 1)
     g.C2 = 2.0 * g.upa0 * g.upa1;
@@ -1201,6 +1240,7 @@ TORJ_HD HarmGeom harm_geom(double mu, double inv_mu, double r, double Npar, doub
     // the threshold's few roundings are ~1e-15 of it, inside the margin of 14)
     const double th = fma(760.0, inv_mu, 1.0);
     g.zero = g.qmin > 1.0 && g.qmin > th * th;
+#endif
     return g;
 }
 
@@ -1247,6 +1287,8 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
     c.C0 = hg.C0;
     c.C1 = hg.C1;
     c.C2 = hg.C2;
+    c.Y0 = hg.Y0;
+    c.Y1 = hg.Y1;
     c.hx = 0.5 * c.x_m;
     c.hx2 = c.hx * c.hx;
     const double qmin = hg.qmin;
@@ -1300,7 +1342,14 @@ TORJ_HD double albajar_harmonic(const GLTable &gl, double mu, const HarmGeom &hg
         for (int k = 1; k < 2 * M - 1; k++) p *= hx;
         const double B0 = 4.0 * mu * (Pm * Pm) * sq_r * p * (Pmax + Qmax);
         const double R = B0 * rcp_nz(fabs(dom));
-#if TORJ_EMAX_BOUND
+#if TORJ_NODE_GAMMA_LIN
+        // E_max <= 2^(ceil(ymax) + 1): every node's y is at most ymax up to its
+        // roundings (a few 1e-13), the extra factor 2 covers them and exp2_node's
+        // 4e-12; a NaN ymax gives an infinite bound, which never skips
+        const double yb = ceil(hg.ymax) + 1.0;
+        const double Emax = ldexp_i(1.0, (int)fmax(fmin(yb, 2000.0), -2000.0));
+        (void)qmin;
+#elif TORJ_EMAX_BOUND
         // an upper bound on E_max = exp(mu (1 - gamma_min)) without the exponential:
         // 2^(ceil(y) + 1) with y = mu log2(e) (1 - gamma_min) from the node loop's
         // square root (a few ulp; the extra factor 2 covers y's rounding, |y| <

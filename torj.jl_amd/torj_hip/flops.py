@@ -15,21 +15,24 @@ from __future__ import annotations
 FLOPS_RHS_COLD = 815        # spline fields + B rotation + analytic dD/dx, dD/dN + Te
 FLOPS_ALPHA_PRE = 83        # abs_Albajar_fast up to the harmonic sum (pol. vector etc.)
 FLOPS_ALPHA_POST = 17       # Maxwellian normalisation + final scaling
-FLOPS_HARM = 46             # per harmonic: K0..K5, C0..C2, u_par coefficients, post-scaling
-FLOPS_PAIR_SHARED = 35      # per +-t node pair: Bessel argument, recurrence, P, Q, combination
-FLOPS_NODE = 30             # per node: gamma^2, sqrt, exponent, exp
+FLOPS_HARM = 40             # per harmonic: K0..K5, the node exponents' Y0 / Y1, post-scaling
+FLOPS_PAIR_SHARED = 32      # per +-t node pair: Bessel argument, recurrence, P, Q, combination
+FLOPS_NODE = 28             # per node: exponent Y0 -+ Y1 t (gamma linear in t, round 6), exp
 FLOPS_SERIES_TERM = 4       # per Horner term (two series, one fma each)
 FLOPS_STEP_OVERHEAD = 234   # RK4 combination, exp(-tau), psi evaluation
-FLOPS_ZERO_TEST = 12        # per harmonic found exactly zero: the gamma_min bound (its setup
-                            # is FLOPS_HARM; the node loop it skips is not counted)
-FLOPS_NEGL_TEST = 59        # per harmonic skipped as below an ulp of the sum (torj_math.hpp
+FLOPS_ZERO_TEST = 1         # per harmonic found exactly zero: the largest node exponent
+                            # Y0 + |Y1| (its setup is FLOPS_HARM; the node loop it skips is not
+                            # counted; round 5: 12 for the gamma_min bound of the quadratic form)
+FLOPS_NEGL_TEST = 35        # per harmonic skipped as below an ulp of the sum (torj_math.hpp
                             # albajar_harmonic): the bound's Bessel/polarisation factors (33),
-                            # exp(mu (1 - gamma_min)) (26 + 3) -- on top of FLOPS_HARM and the
+                            # E_max as 2^(ceil(ymax) + 1) (2; round 5: exp(mu (1 - gamma_min)),
+                            # 26 + 3) -- on top of FLOPS_HARM and the
                             # gamma_min test; the node loop it skips is not counted.  Tests that
                             # do not skip cost the same and are not counted (conservative).
-FLOPS_EARLY_HARM = 27       # per harmonic of a call settled before the polarisation vector
-                            # (torj_math.hpp harm_geom: r, sqrt(r^2 - 1), u_par0/1, C0..C2 (15)
-                            # and the gamma_min test (12)); the call's own prologue
+FLOPS_EARLY_HARM = 12       # per harmonic of a call settled before the polarisation vector
+                            # (torj_math.hpp harm_geom: r, sqrt(r^2 - 1), u_par1, Y0, Y1 (11) and
+                            # the zero test's Y0 + |Y1| (1); round 5: 27 with the quadratic
+                            # form's C0..C2 and gamma_min); the call's own prologue
                             # (mu, omega_bar, N_perp, m_0: 12) is not counted (conservative).
 
 
