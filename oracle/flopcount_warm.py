@@ -143,11 +143,14 @@ def faddeeva_weideman_count():
     ir, ii = dr * idn, -di * idn
     nr, ni = L - y, x
     zr, zi = nr * ir - ni * ii, nr * ii + ni * ir
-    pr, pim = CF(0.1), CF(0.0)
-    for k in range(1, KWEID_N):
-        t = pr * zr + (-pim * zi + 0.01 * k)
-        pim = pr * zi + pim * zr
-        pr = t
+    # weid_poly (round 6): the real-coefficient recurrence b_k = a_k + r b_(k+1) - s b_(k+2)
+    r, s = 2.0 * zr, zr * zr + zi * zi
+    b2 = CF(0.1)
+    b1 = r * b2 + 0.01
+    for k in range(2, KWEID_N - 1):
+        b1, b2 = r * b1 + (-s * b2 + 0.01 * k), b1
+    pr = zr * b1 + (-s * b2 + 0.02)
+    pim = zi * b1
     i2r, i2i = ir * ir - ii * ii, 2.0 * ir * ii
     wr = 2.0 * (pr * i2r - pim * i2i) + 0.5 * ir
     wi = 2.0 * (pr * i2i + pim * i2r) + 0.5 * ii
