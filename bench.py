@@ -52,8 +52,8 @@ FLOP_MODEL = {"albajar": "albajar-v5 (round 6: the node loop's gamma as the reso
                          "negligible ones; round 3: exact-zero, negligible and settled-early harmonics "
                          "priced at their tests)",
               "none": "albajar-v5",
-              "warm_wr": "warm-v4 (round 6: Weideman's polynomial by the real-coefficient recurrence, 176 FLOP "
-                         "per evaluation instead of 278; round 5: warmdisp's breaking pass sums no tensor, its root by "
+              "warm_wr": "warm-v4 (round 6: Weideman's polynomial and the asymptotic series by the real-coefficient "
+                         "recurrence, 176 and 60 FLOP per evaluation instead of 278 and 84; round 5: warmdisp's breaking pass sums no tensor, its root by "
                          "the conjugate product, the asymptotic Faddeeva series by Horner; round 3: counter[2] = asymptotic Faddeeva "
                          "evaluations; larmornumber tests priced at one per call, a lower bound)"}
 ALPHA_NAME = {"none": "no absorption (cold)", "albajar": "Albajar alpha (GL-24)",

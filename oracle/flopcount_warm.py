@@ -23,7 +23,8 @@ dependent parts are counted at their cheapest branch (a lower bound):
   updates) are counted with 99.
 The Faddeeva value comes from scipy; its op count is that of the branch the
 kernel runs (torj_warm.hpp faddeeva_upper): the asymptotic series (10 terms)
-where |x| >= 16 or Im z >= 16, else Weideman's N = 36 complex Horner sum.  The
+where |x| >= 16 or Im z >= 16, else Weideman's N = 36 sum (both by the
+real-coefficient recurrence since round 6, complex Horner before).  The
 model prices larmornumber's resonance tests at one per call (their least).
 """
 from __future__ import annotations
@@ -169,10 +170,15 @@ def faddeeva_asym_count():
     ir2 = 1.0 / (x * x + y * y)
     a, b = x * ir2, -y * ir2
     ur, ui = 0.5 * (a * a - b * b), a * b
-    # Horner in u with the (2k - 1)!! as constants (torj_warm.hpp faddeeva_asym)
-    tr, ti = CF(34459425.0), CF(0.0)
-    for k in range(KFAD_ASYM_K - 2, -1, -1):
-        tr, ti = tr * ur + (-ti * ui + float(math.prod(range(1, 2 * k, 2)))), tr * ui + ti * ur
+    # the (2k - 1)!! series in u by Knuth's real-coefficient recurrence (torj_warm.hpp
+    # asym_horner, TORJ_ASYM_KNUTH, round 6; complex Horner before)
+    df = lambda k: float(math.prod(range(1, 2 * k, 2)))  # noqa: E731
+    r, s = 2.0 * ur, ur * ur + ui * ui
+    b2 = CF(df(KFAD_ASYM_K - 1))
+    b1 = r * b2 + df(KFAD_ASYM_K - 2)
+    for k in range(KFAD_ASYM_K - 3, 0, -1):
+        b1, b2 = r * b1 + (-s * b2 + df(k)), b1
+    tr, ti = ur * b1 + (-s * b2 + 1.0), ui * b1
     pr, pim = a * tr - b * ti, a * ti + b * tr
     _ = (-0.56 * pim, 0.56 * pr)
     _ = (-1.77 * _[1], 1.77 * _[0])

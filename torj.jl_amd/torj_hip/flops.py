@@ -82,7 +82,7 @@ def algorithmic_flops_reference(counters, n_gl: int = 24) -> float:
 FLOPS_WARM_CALL = 80          # Te, |N|, mu, N_perp, per-call invariants, e330, alpha
 FLOPS_WARM_LARMOR_TEST = 10   # per larmornumber resonance test
 FLOPS_WARM_FADDEEVA = 176     # per Z(z) by Weideman's N = 36 sum (|z| < 16) by the real-coefficient recurrence (round 6; 278 by complex Horner)
-FLOPS_WARM_FADDEEVA_ASYM = 84   # per Z(z) by the asymptotic series (|x| or Im z >= 16), 10 terms, Horner
+FLOPS_WARM_FADDEEVA_ASYM = 60   # per Z(z) by the asymptotic series (|x| or Im z >= 16), 10 terms by the real-coefficient recurrence (round 6; 84 by complex Horner)
 FLOPS_WARM_SIDE = 14          # per fsup side s = +-|s|: alpha_s, phi, cf12, cf32
 FLOPS_WARM_STEP = 6           # per Shkarofsky recursion step
 FLOPS_WARM_STORE = 4          # per stored recursion step: cefp, cefm accumulation
