@@ -598,6 +598,18 @@ def main_library(args):
     flop0 = (F.algorithmic_flops(cnt[0], n_gl=24) if args.absorption in ("albajar", "none")
              else F.algorithmic_flops_warm(cnt[0]) if args.absorption == "warm_wr" else None)
     achieved = flop0 / (kern_ms / 1e3) / 1e12 if flop0 is not None and kern_ms > 0 else None
+    # device 0's launch is the profiled single-device workload when each device
+    # traces the whole fan (weak scaling): its HBM bytes per launch from the
+    # profile of the same build, workload and switches (None otherwise, e.g. for
+    # the C4 shards, which no profile covers)
+    traffic0 = None
+    if args.absorption in ("albajar", "warm_wr"):
+        try:
+            kn = SPLIT_KERNELS if args.absorption == "albajar" else SPLIT_KERNELS.replace("k_alpha_pts",
+                                                                                            "k_alpha_warm_pts")
+            traffic0 = measured_traffic(kn, int(shards[0]["n"]), args, L.torj_build_id().decode())
+        except Exception:  # a missing or malformed profile leaves the field empty
+            traffic0 = None
     dP0 = shards[0]["dP_shell"].cpu().numpy()
     agree = max(float(np.abs(sh["dP_shell"].cpu().numpy() - dP0).max()) for sh in shards)
     placement = ("same-device rehearsal (TORJ_BEAM_SAME_DEVICE=1): all replicas on device 0, partials "
@@ -643,7 +655,10 @@ def main_library(args):
             "peak": FP64_VECTOR_PEAK_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / FP64_VECTOR_PEAK_TFLOPS if achieved is not None else None,
-            "traffic": None,
+            "traffic": traffic0["traffic_bytes"] if traffic0 else None,
+            "traffic_source": ((traffic0["file"] + ": the single-device profile of device 0's launch "
+                                "(same build, rays, steps and switches), not measured in this run")
+                               if traffic0 else None),
             "note": "device 0's trace phase (library HIP events) and its shard's counted FLOPs",
             "kernel_ms": kern_ms,
             "deposition_kernels_ms": post_ms,
@@ -903,6 +918,15 @@ def torj_env():
             if k.startswith("TORJ_") and k != "TORJ_HIP_LIB"}  # the library: its build id
 
 
+# switches that place replicas / ranks on devices without changing any kernel:
+# not part of the match between a run and a profile
+PLACEMENT_ENV = ("TORJ_BENCH_SAME_DEVICE", "TORJ_BEAM_SAME_DEVICE")
+
+
+def kernel_env(env):
+    return {k: v for k, v in env.items() if k not in PLACEMENT_ENV}
+
+
 def measured_traffic(kname, n, args, build_id):
     """HBM bytes per launch of the hot kernel, measured offline by
     scripts/profile.sh (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, gfx950
@@ -919,7 +943,7 @@ def measured_traffic(kname, n, args, build_id):
         except (OSError, ValueError):
             continue
         wl = t.get("workload", {})
-        if (wl.get("build_id") == build_id and wl.get("torj_env", {}) == torj_env()
+        if (wl.get("build_id") == build_id and kernel_env(wl.get("torj_env", {})) == kernel_env(torj_env())
                 and base in (t.get("kernel") or "") and wl.get("rays") == n
                 and wl.get("rk4_steps") == args.n_steps and wl.get("n_psi") == args.n_psi
                 and wl.get("traj_stride") == args.traj_stride

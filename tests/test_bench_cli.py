@@ -149,3 +149,36 @@ def test_tiny_alpha_and_resolvable_tau_statistic(monkeypatch):
         assert c["out_of_bar"][0]["fan_index"] == 2
         want = 1e-12 if flagged else 6e-10
         assert abs(c["max_rel_tau_resolvable_excl_flagged"] - want) < 0.1 * want
+
+
+def test_traffic_profile_match_ignores_placement_switches(monkeypatch):
+    """measured_traffic pairs a run with a committed profile of the same build,
+    workload and kernel switches; the placement-only switches of the same-device
+    rehearsals (TORJ_BEAM_SAME_DEVICE, TORJ_BENCH_SAME_DEVICE) do not enter the
+    match, any kernel switch does (CPU: the profile files only)."""
+    import glob
+    import importlib.util
+    import json
+
+    f = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "traffic.json")))[-1]
+    wl = json.load(open(f))["workload"]
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    B = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(B)
+
+    class A:
+        n_steps, n_psi, traj_stride, absorption = wl["rk4_steps"], wl["n_psi"], wl["traj_stride"], "albajar"
+
+    for k in list(os.environ):
+        if k.startswith("TORJ_"):
+            monkeypatch.delenv(k)
+    for k, v in wl.get("torj_env", {}).items():
+        monkeypatch.setenv(k, v)
+    t = B.measured_traffic(B.SPLIT_KERNELS, wl["rays"], A, wl["build_id"])
+    assert t is not None and t["traffic_bytes"] > 0
+    monkeypatch.setenv("TORJ_BEAM_SAME_DEVICE", "1")
+    monkeypatch.setenv("TORJ_BENCH_SAME_DEVICE", "1")
+    assert B.measured_traffic(B.SPLIT_KERNELS, wl["rays"], A, wl["build_id"]) is not None
+    monkeypatch.setenv("TORJ_ALPHA_ZFLAG", "0")  # a kernel switch: no match
+    assert B.measured_traffic(B.SPLIT_KERNELS, wl["rays"], A, wl["build_id"]) is None
+    assert B.measured_traffic(B.SPLIT_KERNELS, wl["rays"], A, "0" * 16) is None
