@@ -1407,19 +1407,15 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
     const int i = q * kAlphaBlock + threadIdx.x;
     if (i >= a.n) return;
     const int j = js >> 2;
-    // every load of the point at once (one memory latency, not three in a
-    // row): the stop words and the inputs, whose addresses are valid for any
-    // i < n whether or not the point is live
+    // the stop words and the block's zero flag first
     const int ti = sp.tinfo[i], si = sp.sinfo[i];
     const int zf = sp.zflag ? sp.zflag[i] : 0;
-    const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
-    const double X = in[0], Y = in[(size_t)a.n], N2 = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
-    const double lnTe = in[4 * (size_t)a.n];
-    // (an empty asm that consumes them: the compiler would otherwise sink the
-    // input loads below the stop test and the Te test, three latencies in a row)
-    asm volatile("" ::"v"(ti), "v"(si), "v"(zf), "v"(X), "v"(Y), "v"(N2), "v"(Npar), "v"(lnTe));
     // the trajectory kernel's block zero flags: a wave whose rays all carry one
     // writes 0 (abs_albajar_fast_body's early settle returns +0 there) and ends
+    // before its input loads are issued (round 6: waiting for the five inputs
+    // too, as below, cost the flagged 39 % of the waves a memory latency and
+    // ~12 GB of reads per launch; C3 trace -1.2 ms alternating,
+    // profiles/r06/ab_log.txt r6zff)
     if (__all(zf != 0)) {
 #if defined(TORJ_ALPHA_PROF) && defined(__HIP_DEVICE_COMPILE__)
         TORJ_APROF_WAVE(kAprofZ);
@@ -1428,6 +1424,14 @@ __global__ void __launch_bounds__(kAlphaBlock, TORJ_ALPHA_WAVES) k_alpha_pts(Tra
         if constexpr (COUNT) sp.awork[(size_t)js * a.n + i] = 0u;
         return;
     }
+    // the five inputs at once (one memory latency, not three in a row; their
+    // addresses are valid for any i < n whether or not the point is live)
+    const double *in = sp.ain + (size_t)js * sp.nf * a.n + i;
+    const double X = in[0], Y = in[(size_t)a.n], N2 = in[2 * (size_t)a.n], Npar = in[3 * (size_t)a.n];
+    const double lnTe = in[4 * (size_t)a.n];
+    // (an empty asm that consumes them: the compiler would otherwise sink the
+    // input loads below the stop test and the Te test, three latencies in a row)
+    asm volatile("" ::"v"(ti), "v"(si), "v"(X), "v"(Y), "v"(N2), "v"(Npar), "v"(lnTe));
     // sinfo may be stale (k_tau_scan of an earlier block runs on another
     // stream): an optimisation only, as in traj_body -- a stale OK evaluates an
     // alpha the scan never reads
